@@ -1,0 +1,217 @@
+"""ORACLE (test infrastructure only) — ctypes front-end of ``oracle/libmforacle.so``.
+
+Exposes the C restatement (``oracle/mf_oracle.c``) to tests and to bench.py's
+``cpu_baseline`` leg.  Builds the model blob from the numpy URDF restatement
+(``oracle/urdf_np.py``), i.e. completely independently of the product's C++
+URDF parser.  Nothing in ``mpc_fatigue_amd`` imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from .urdf_np import Model
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libmforacle.so")
+MJ = 16
+BLOB_HDR = 4
+BLOB_JSTRIDE = 33
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "mf_oracle.c")):
+        subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB)
+        dp = C.POINTER(C.c_double)
+        L.mfo_id.argtypes = [dp, dp, dp, dp, dp]
+        L.mfo_fk.argtypes = [dp, dp, dp, dp, dp]
+        L.mfo_jac.argtypes = [dp, dp, dp, dp]
+        L.mfo_solve.argtypes = [dp, C.POINTER(OCP), C.POINTER(Opts), dp, C.POINTER(Result)]
+        L.mfo_solve_batch.argtypes = [dp, C.POINTER(OCP), C.c_int, C.POINTER(Opts), dp, C.c_int,
+                                      C.POINTER(Result), C.c_int]
+        L.mfo_node_derivs.argtypes = [dp, C.POINTER(OCP)] + [dp] * 10
+        _lib = L
+    return _lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def model_blob(model: Model) -> np.ndarray:
+    """Flat model description (layout: include/mpcfatigue.h, MF_BLOB_*)."""
+    n = model.nq
+    b = np.zeros(BLOB_HDR + BLOB_JSTRIDE * n)
+    b[0] = n
+    b[1:4] = model.gravity
+    for j, jt in enumerate(model.joints):
+        if jt.jtype != "revolute":
+            raise ValueError("oracle C path supports revolute joints")
+        o = BLOB_HDR + BLOB_JSTRIDE * j
+        b[o] = jt.parent
+        b[o + 1:o + 10] = jt.R.reshape(-1)
+        b[o + 10:o + 13] = jt.t
+        b[o + 13:o + 16] = jt.axis
+        b[o + 16] = jt.inertia.m
+        b[o + 17:o + 20] = jt.inertia.c
+        b[o + 20:o + 29] = jt.inertia.Ic.reshape(-1)
+        b[o + 29:o + 33] = [jt.lower, jt.upper, jt.effort, jt.velocity]
+    return b
+
+
+def frame_arr(model: Model, name: str) -> np.ndarray:
+    f = model.frames[name]
+    return np.concatenate([[f.parent], f.R.reshape(-1), f.t])
+
+
+class OCP(C.Structure):
+    _fields_ = [
+        ("N", C.c_int), ("nf", C.c_int), ("use_line", C.c_int),
+        ("h", C.c_double),
+        ("frame", C.c_double * 13),
+        ("fdir", C.c_double * 9),
+        ("line_ref", C.c_double * 2),
+        ("wF", C.c_double), ("wqd", C.c_double), ("wtau", C.c_double),
+        ("q0", C.c_double * MJ), ("qd0", C.c_double * MJ),
+        ("qd_lo", C.c_double * MJ), ("qd_hi", C.c_double * MJ),
+        ("q_lo", C.c_double * MJ), ("q_hi", C.c_double * MJ),
+        ("tau_lo", C.POINTER(C.c_double)), ("tau_hi", C.POINTER(C.c_double)),
+    ]
+
+
+class Opts(C.Structure):
+    _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
+                ("mu_init", C.c_double), ("init_zero", C.c_int), ("verbose", C.c_int),
+                ("prox", C.c_double), ("F_init", C.c_double)]
+
+
+class Result(C.Structure):
+    _fields_ = [("status", C.c_int), ("iter", C.c_int), ("kkt", C.c_double), ("cviol", C.c_double),
+                ("obj", C.c_double), ("mu", C.c_double), ("n_ls_fail", C.c_int), ("n_inertia_fix", C.c_int)]
+
+
+def make_ocp(spec: dict, model: Model):
+    """spec: dict produced by ``oracle.problems`` (plain numbers / arrays)."""
+    n = model.nq
+    o = OCP()
+    o.N = spec["N"]
+    o.nf = spec["nf"]
+    o.use_line = int(spec["use_line"])
+    o.h = spec["h"]
+    o.frame[:] = list(frame_arr(model, spec["frame"]))
+    fd = np.zeros(9)
+    fd[:3 * spec["nf"]] = np.asarray(spec["fdir"], float).reshape(-1)
+    o.fdir[:] = list(fd)
+    o.line_ref[:] = list(spec.get("line_ref", [0.0, 0.0]))
+    o.wF, o.wqd, o.wtau = spec["wF"], spec["wqd"], spec["wtau"]
+
+    def arr(v, fill):
+        a = np.full(MJ, fill, float)
+        a[:n] = np.broadcast_to(np.asarray(v, float), (n,))
+        return list(a)
+
+    o.q0[:] = arr(spec["q0"], 0.0)
+    o.qd0[:] = arr(spec.get("qd0", 0.0), 0.0)
+    o.qd_lo[:] = arr(spec["qd_lo"], -np.inf)
+    o.qd_hi[:] = arr(spec["qd_hi"], np.inf)
+    o.q_lo[:] = arr(spec["q_lo"], -np.inf)
+    o.q_hi[:] = arr(spec["q_hi"], np.inf)
+    tl = np.ascontiguousarray(np.broadcast_to(np.asarray(spec["tau_lo"], float), (spec["N"], n)))
+    th = np.ascontiguousarray(np.broadcast_to(np.asarray(spec["tau_hi"], float), (spec["N"], n)))
+    o._keep = (tl, th)
+    o.tau_lo = _p(tl)
+    o.tau_hi = _p(th)
+    return o
+
+
+def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=200, mu_init=0.1, init_zero=False, verbose=False, prox=0.0,
+         F_init=0.0):
+    return Opts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), prox, F_init)
+
+
+def w_size(spec: dict, n: int) -> int:
+    return n + spec["N"] * (2 * n + spec["nf"])
+
+
+def solve(model: Model, spec: dict, **kw):
+    L = lib()
+    blob = model_blob(model)
+    o = make_ocp(spec, model)
+    op = opts(**kw)
+    w = np.zeros(w_size(spec, model.nq))
+    r = Result()
+    err = L.mfo_solve(_p(blob), C.byref(o), C.byref(op), _p(w), C.byref(r))
+    if err:
+        raise RuntimeError(f"mfo_solve error {err}")
+    return w, r
+
+
+def solve_batch(model: Model, specs: list[dict], nthreads: int = 0, **kw):
+    L = lib()
+    blob = model_blob(model)
+    ocps = (OCP * len(specs))()
+    keep = []
+    for i, s in enumerate(specs):
+        o = make_ocp(s, model)
+        keep.append(o._keep)
+        ocps[i] = o
+    op = opts(**kw)
+    ws = w_size(specs[0], model.nq)
+    w = np.zeros((len(specs), ws))
+    res = (Result * len(specs))()
+    err = L.mfo_solve_batch(_p(blob), ocps, len(specs), C.byref(op), _p(w), ws, res, nthreads)
+    if err:
+        raise RuntimeError(f"mfo_solve_batch error {err}")
+    return w, list(res)
+
+
+def inverse_dynamics(model: Model, q, qd, qdd):
+    b = model_blob(model)
+    q, qd, qdd = (np.ascontiguousarray(x, float) for x in (q, qd, qdd))
+    tau = np.zeros(model.nq)
+    lib().mfo_id(_p(b), _p(q), _p(qd), _p(qdd), _p(tau))
+    return tau
+
+
+def forward_kinematics(model: Model, q, frame: str):
+    b = model_blob(model)
+    f = frame_arr(model, frame)
+    q = np.ascontiguousarray(q, float)
+    pos, rot = np.zeros(3), np.zeros(9)
+    lib().mfo_fk(_p(b), _p(f), _p(q), _p(pos), _p(rot))
+    return pos, rot.reshape(3, 3)
+
+
+def jacobian(model: Model, q, frame: str):
+    b = model_blob(model)
+    f = frame_arr(model, frame)
+    q = np.ascontiguousarray(q, float)
+    J = np.zeros(6 * model.nq)
+    lib().mfo_jac(_p(b), _p(f), _p(q), _p(J))
+    return J.reshape(6, model.nq)
+
+
+def node_derivs(model: Model, spec: dict, q, qd, F, cw, yl):
+    n = model.nq
+    nf = spec["nf"]
+    nv = 2 * n + nf
+    o = make_ocp(spec, model)
+    b = model_blob(model)
+    arrs = [np.ascontiguousarray(x, float) for x in (q, qd, F, cw, yl)]
+    tau, Jt, pf, Jp, H = np.zeros(n), np.zeros(n * nv), np.zeros(3), np.zeros(3 * n), np.zeros(nv * nv)
+    lib().mfo_node_derivs(_p(b), C.byref(o), *[_p(a) for a in arrs], _p(tau), _p(Jt), _p(pf), _p(Jp), _p(H))
+    return tau, Jt.reshape(n, nv), pf, Jp.reshape(3, n), H.reshape(nv, nv)
