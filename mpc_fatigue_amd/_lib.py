@@ -1,0 +1,151 @@
+"""ctypes binding of libmpcfatigue.so (C ABI: include/mpcfatigue.h).
+
+The library is built in-tree (``mpc_fatigue_amd/libmpcfatigue.so``) by
+``build()`` / ``make -C mpc_fatigue_amd``.  There is deliberately no CPU
+fallback: if the shared object is missing, or the process has no HIP device,
+every compute call raises ``MFError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmpcfatigue.so")
+MF_MAX_JOINTS = 16
+
+MF_ERR = {0: "OK", -1: "ARG", -2: "URDF", -3: "FRAME", -4: "DEVICE", -5: "UNSUPPORTED", -6: "NOMEM"}
+
+
+class MFError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libmpcfatigue error {code} ({MF_ERR.get(code, '?')}): {msg}")
+        self.code = code
+
+
+def build(force: bool = False) -> str:
+    """Compile libmpcfatigue.so for gfx950 with hipcc (in-tree)."""
+    args = ["make", "-s", "-C", HERE, "-j4"]
+    if force:
+        subprocess.check_call(["make", "-s", "-C", HERE, "clean"])
+    subprocess.check_call(args)
+    return LIB_PATH
+
+
+class ProblemSpec(C.Structure):
+    _fields_ = [
+        ("N", C.c_int), ("h", C.c_double), ("frame", C.c_int), ("nf", C.c_int),
+        ("fdir", C.c_double * 9), ("use_line", C.c_int), ("line_ref", C.c_double * 2),
+        ("wF", C.c_double), ("wqd", C.c_double), ("wtau", C.c_double),
+        ("qd0", C.c_double * MF_MAX_JOINTS),
+        ("qd_lo", C.c_double * MF_MAX_JOINTS), ("qd_hi", C.c_double * MF_MAX_JOINTS),
+        ("q_lo", C.c_double * MF_MAX_JOINTS), ("q_hi", C.c_double * MF_MAX_JOINTS),
+        ("tau_lo", C.POINTER(C.c_double)), ("tau_hi", C.POINTER(C.c_double)),
+    ]
+
+
+class SolverOpts(C.Structure):
+    _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
+                ("mu_init", C.c_double), ("F_init", C.c_double), ("verbose", C.c_int)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MFError(-4, f"{LIB_PATH} not built (run __graft_entry__.build() or make -C mpc_fatigue_amd)")
+    L = C.CDLL(LIB_PATH)
+    vp, dp, ip, cp = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_char_p
+    sig = {
+        "mf_model_from_urdf": ([cp, C.POINTER(vp)], C.c_int),
+        "mf_model_free": ([vp], None),
+        "mf_model_nq": ([vp], C.c_int),
+        "mf_model_export": ([vp, dp, C.c_int], C.c_int),
+        "mf_frame_id": ([vp, cp], C.c_int),
+        "mf_frame_export": ([vp, C.c_int, dp], C.c_int),
+        "mf_id": ([vp, dp, dp, dp, dp, C.c_int], C.c_int),
+        "mf_fk": ([vp, C.c_int, dp, dp, dp, C.c_int], C.c_int),
+        "mf_jac": ([vp, C.c_int, dp, dp, C.c_int], C.c_int),
+        "mf_id_dev": ([vp, vp, vp, vp, vp, C.c_int, vp], C.c_int),
+        "mf_fk_dev": ([vp, C.c_int, vp, vp, vp, C.c_int, vp], C.c_int),
+        "mf_jac_dev": ([vp, C.c_int, vp, vp, C.c_int, vp], C.c_int),
+        "mf_problem_create": ([vp, C.POINTER(ProblemSpec), C.POINTER(vp)], C.c_int),
+        "mf_problem_free": ([vp], None),
+        "mf_problem_wsize": ([vp], C.c_int),
+        "mf_node_eval": ([vp, dp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
+        "mf_solve_batch": ([vp, C.c_int, dp, dp, C.POINTER(SolverOpts), dp, ip, ip, dp, dp, C.c_int], C.c_int),
+        "mf_solve_batch_dev": ([vp, C.c_int, vp, vp, C.POINTER(SolverOpts), vp, vp, vp, vp, vp, vp], C.c_int),
+        "mf_last_error": ([], cp),
+    }
+    for name, (argt, rest) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = argt
+        fn.restype = rest
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = [
+    "mf_model_from_urdf", "mf_model_free", "mf_model_nq", "mf_model_export", "mf_frame_id", "mf_frame_export",
+    "mf_id", "mf_fk", "mf_jac", "mf_id_dev", "mf_fk_dev", "mf_jac_dev", "mf_problem_create", "mf_problem_free",
+    "mf_problem_wsize", "mf_node_eval", "mf_solve_batch", "mf_solve_batch_dev", "mf_last_error",
+]
+
+
+def check(code: int) -> int:
+    if code < 0:
+        msg = lib().mf_last_error()
+        raise MFError(code, msg.decode() if msg else "")
+    return code
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+class Model:
+    """Owning handle of an ``mf_model`` (URDF → kinematic tree, Pinocchio semantics)."""
+
+    def __init__(self, urdf_xml: str):
+        h = C.c_void_p()
+        check(lib().mf_model_from_urdf(urdf_xml.encode(), C.byref(h)))
+        self._h = h
+        self.nq = lib().mf_model_nq(h)
+        self.nv = self.nq
+
+    @property
+    def handle(self):
+        return self._h
+
+    def frame_id(self, name: str) -> int:
+        return check(lib().mf_frame_id(self._h, name.encode()))
+
+    def export(self) -> np.ndarray:
+        need = check(lib().mf_model_export(self._h, None, 0))
+        b = np.zeros(need)
+        lib().mf_model_export(self._h, dptr(b), need)
+        return b
+
+    def frame_record(self, frame: int) -> np.ndarray:
+        r = np.zeros(13)
+        check(lib().mf_frame_export(self._h, frame, dptr(r)))
+        return r
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.mf_model_free(h)
+            self._h = None

@@ -1,0 +1,646 @@
+// extern "C" ABI of libmpcfatigue.so (declared in include/mpcfatigue.h).
+//
+// Host side: URDF ingestion (urdf.cpp), device model images, problem objects
+// and the batched solve driver.  Device side: the bridge kernels below
+// (inverse dynamics / FK / frame Jacobian, one lane per sample) and the
+// interior-point kernels in ipm_kernels.hip.  There is no CPU compute path:
+// without a usable device every compute entry point fails with MF_ERR_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <string>
+#include <vector>
+
+#include "dyn.hpp"
+#include "ipm.hpp"
+#include "model.hpp"
+
+namespace mf {
+bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevFrame *F, const OcpConst &C,
+                  const IpmArrays &A, int batch, hipStream_t s, double *w, int *status, int *iters, double *kkt,
+                  double *obj);
+}
+
+using namespace mf;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+extern "C" const char *mf_last_error(void) { return g_err.c_str(); }
+
+#define HIPCHK(x)                                                                                     \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) return fail(MF_ERR_DEVICE, std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+    } while (0)
+
+static int ensure_device() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) return fail(MF_ERR_DEVICE, "no HIP device available (libmpcfatigue has no CPU path)");
+    return MF_OK;
+}
+
+namespace mf {
+DevModel make_dev_model(const Model &M) {
+    DevModel D;
+    memset(&D, 0, sizeof D);
+    D.n = (int)M.joints.size();
+    D.serial = 1;
+    for (int k = 0; k < 3; k++) D.g[k] = M.gravity[k];
+    for (int i = 0; i < D.n; i++) {
+        const Joint &J = M.joints[i];
+        DevJoint &d = D.j[i];
+        memcpy(d.RX, J.R, sizeof d.RX);
+        memcpy(d.tX, J.t, sizeof d.tX);
+        memcpy(d.axis, J.axis, sizeof d.axis);
+        const double *a = J.axis;
+        double K[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
+        memcpy(d.K, K, sizeof K);
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) d.K2[3 * r + c] = K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c] + K[3 * r + 2] * K[6 + c];
+        d.m = J.mass;
+        memcpy(d.c, J.com, sizeof d.c);
+        memcpy(d.Ic, J.Ic, sizeof d.Ic);
+        d.parent = J.parent;
+        if (J.parent != i - 1) D.serial = 0;
+    }
+    return D;
+}
+DevFrame make_dev_frame(const Model &M, int frame) {
+    DevFrame F;
+    memset(&F, 0, sizeof F);
+    const Frame &f = M.frames[frame];
+    F.parent = f.parent;
+    memcpy(F.R, f.R, sizeof F.R);
+    memcpy(F.t, f.t, sizeof F.t);
+    return F;
+}
+}  // namespace mf
+
+struct mf_model {
+    Model host;
+    DevModel dev;
+    DevModel *d_model = nullptr;
+    std::vector<DevFrame *> d_frames;  // lazily uploaded
+};
+
+static int upload_model(mf_model *m) {
+    if (m->d_model) return MF_OK;
+    int e = ensure_device();
+    if (e) return e;
+    HIPCHK(hipMalloc(&m->d_model, sizeof(DevModel)));
+    HIPCHK(hipMemcpy(m->d_model, &m->dev, sizeof(DevModel), hipMemcpyHostToDevice));
+    m->d_frames.assign(m->host.frames.size(), nullptr);
+    return MF_OK;
+}
+static int frame_dev(mf_model *m, int frame, DevFrame **out) {
+    int e = upload_model(m);
+    if (e) return e;
+    if (frame < 0 || frame >= (int)m->host.frames.size()) return fail(MF_ERR_FRAME, "frame index out of range");
+    if (!m->d_frames[frame]) {
+        DevFrame F = make_dev_frame(m->host, frame);
+        HIPCHK(hipMalloc(&m->d_frames[frame], sizeof(DevFrame)));
+        HIPCHK(hipMemcpy(m->d_frames[frame], &F, sizeof F, hipMemcpyHostToDevice));
+    }
+    *out = m->d_frames[frame];
+    return MF_OK;
+}
+
+extern "C" int mf_model_from_urdf(const char *urdf_xml, mf_model **out) {
+    if (!urdf_xml || !out) return fail(MF_ERR_ARG, "null argument");
+    try {
+        mf_model *m = new mf_model();
+        m->host = build_model_from_urdf(urdf_xml);
+        m->dev = make_dev_model(m->host);
+        *out = m;
+        return MF_OK;
+    } catch (const std::exception &ex) {
+        return fail(MF_ERR_URDF, ex.what());
+    }
+}
+
+extern "C" void mf_model_free(mf_model *m) {
+    if (!m) return;
+    if (m->d_model) (void)hipFree(m->d_model);
+    for (auto *f : m->d_frames)
+        if (f) (void)hipFree(f);
+    delete m;
+}
+
+extern "C" int mf_model_nq(const mf_model *m) { return m ? (int)m->host.joints.size() : MF_ERR_ARG; }
+
+extern "C" int mf_model_export(const mf_model *m, double *blob, int cap) {
+    if (!m) return fail(MF_ERR_ARG, "null model");
+    int n = (int)m->host.joints.size();
+    int need = MF_BLOB_HDR + MF_BLOB_JSTRIDE * n;
+    std::vector<double> b(need, 0.0);
+    b[0] = n;
+    for (int k = 0; k < 3; k++) b[1 + k] = m->host.gravity[k];
+    for (int j = 0; j < n; j++) {
+        const Joint &J = m->host.joints[j];
+        double *o = b.data() + MF_BLOB_HDR + MF_BLOB_JSTRIDE * j;
+        o[0] = J.parent;
+        memcpy(o + 1, J.R, 9 * sizeof(double));
+        memcpy(o + 10, J.t, 3 * sizeof(double));
+        memcpy(o + 13, J.axis, 3 * sizeof(double));
+        o[16] = J.mass;
+        memcpy(o + 17, J.com, 3 * sizeof(double));
+        memcpy(o + 20, J.Ic, 9 * sizeof(double));
+        o[29] = J.lower; o[30] = J.upper; o[31] = J.effort; o[32] = J.velocity;
+    }
+    if (blob) memcpy(blob, b.data(), sizeof(double) * (size_t)(cap < need ? cap : need));
+    return need;
+}
+
+extern "C" int mf_frame_id(const mf_model *m, const char *name) {
+    if (!m || !name) return fail(MF_ERR_ARG, "null argument");
+    for (size_t i = 0; i < m->host.frames.size(); i++)
+        if (m->host.frames[i].name == name) return (int)i;
+    return fail(MF_ERR_FRAME, std::string("unknown frame '") + name + "'");
+}
+
+extern "C" int mf_frame_export(const mf_model *m, int frame, double *rec13) {
+    if (!m || !rec13) return fail(MF_ERR_ARG, "null argument");
+    if (frame < 0 || frame >= (int)m->host.frames.size()) return fail(MF_ERR_FRAME, "frame index out of range");
+    const Frame &f = m->host.frames[frame];
+    rec13[0] = f.parent;
+    memcpy(rec13 + 1, f.R, 9 * sizeof(double));
+    memcpy(rec13 + 10, f.t, 3 * sizeof(double));
+    return MF_OK;
+}
+
+// ====================================================================== bridge kernels
+// One lane per sample; runtime n <= MF_MAX_JOINTS (these are the drop-in numeric calls,
+// not the solver hot loop).
+template <int NJ>
+__global__ __launch_bounds__(256) void k_bridge_id(const DevModel *__restrict__ Mg, const double *q, const double *qd,
+                                                   const double *qdd, double *tau, int batch) {
+    __shared__ DevModel M;
+    {
+        const double *s = reinterpret_cast<const double *>(Mg);
+        double *d = reinterpret_cast<double *>(&M);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevModel) / sizeof(double)); i += blockDim.x) d[i] = s[i];
+    }
+    __syncthreads();
+    int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    const int n = M.n;
+    double xq[NJ], xqd[NJ], xqdd[NJ];
+    for (int i = 0; i < n; i++) { xq[i] = q[b * n + i]; xqd[i] = qd[b * n + i]; xqdd[i] = qdd[b * n + i]; }
+    TotVis<double> tv;
+    tv.F = nullptr;
+    tv.init();
+    ne_pass<double>(M, n, xq, xqd, xqdd, tv);
+    EmitVis<double, NJ> ev;
+    ev.tot = &tv;
+    ev.fp = -1;
+    for (int k = 0; k < 3; k++) ev.Fw[k] = 0.0;
+    ev.init();
+    ne_pass<double>(M, n, xq, xqd, xqdd, ev);
+    for (int i = 0; i < n; i++) tau[b * n + i] = ev.tau[i];
+}
+
+template <int NJ>
+__global__ __launch_bounds__(256) void k_bridge_kin(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                                    const double *q, double *pos, double *rot, double *J, int batch) {
+    __shared__ DevModel M;
+    __shared__ DevFrame F;
+    {
+        const double *s = reinterpret_cast<const double *>(Mg);
+        double *d = reinterpret_cast<double *>(&M);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevModel) / sizeof(double)); i += blockDim.x) d[i] = s[i];
+        const double *s2 = reinterpret_cast<const double *>(Fg);
+        double *d2 = reinterpret_cast<double *>(&F);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevFrame) / sizeof(double)); i += blockDim.x) d2[i] = s2[i];
+    }
+    __syncthreads();
+    int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    const int n = M.n;
+    double xq[NJ], zero[NJ];
+    for (int i = 0; i < n; i++) { xq[i] = q[b * n + i]; zero[i] = 0.0; }
+    JacVis<double, NJ> jv;
+    jv.F = &F;
+    if (F.parent < 0) {
+        for (int k = 0; k < 3; k++) jv.pf[k] = F.t[k];
+        for (int k = 0; k < 9; k++) jv.Rf[k] = F.R[k];
+    }
+    ne_pass<double>(M, n, xq, zero, (const double *)nullptr, jv);
+    if (pos)
+        for (int k = 0; k < 3; k++) pos[b * 3 + k] = jv.pf[k];
+    if (rot)
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) rot[b * 9 + c * 3 + r] = jv.Rf[r * 3 + c];
+    if (J) {
+        double *Jb = J + (size_t)b * 6 * n;
+        for (int j = 0; j < n; j++) {
+            bool anc = false;
+            for (int a = F.parent; a >= 0; a = M.j[a].parent)
+                if (a == j) { anc = true; break; }
+            double lin[3] = {0, 0, 0}, ang[3] = {0, 0, 0};
+            if (anc) {
+                double d[3] = {jv.pf[0] - jv.o[j][0], jv.pf[1] - jv.o[j][1], jv.pf[2] - jv.o[j][2]};
+                cross3(lin, jv.z[j], d);
+                for (int k = 0; k < 3; k++) ang[k] = jv.z[j][k];
+            }
+            for (int k = 0; k < 3; k++) { Jb[j * 6 + k] = lin[k]; Jb[j * 6 + 3 + k] = ang[k]; }
+        }
+    }
+}
+
+static int check_serial(const mf_model *m) {
+    if (!m->dev.serial) return fail(MF_ERR_UNSUPPORTED, "branching kinematic trees are not supported by the kernels yet");
+    return MF_OK;
+}
+
+extern "C" int mf_id_dev(const mf_model *mc, const double *q, const double *qd, const double *qdd, double *tau,
+                         int batch, void *stream) {
+    mf_model *m = const_cast<mf_model *>(mc);
+    if (!m || batch < 0) return fail(MF_ERR_ARG, "bad argument");
+    int e = check_serial(m);
+    if (e) return e;
+    if ((e = upload_model(m))) return e;
+    if (batch == 0) return MF_OK;
+    hipLaunchKernelGGL(k_bridge_id<MF_MAX_JOINTS>, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       m->d_model, q, qd, qdd, tau, batch);
+    HIPCHK(hipGetLastError());
+    return MF_OK;
+}
+
+static int kin_dev(const mf_model *mc, int frame, const double *q, double *pos, double *rot, double *J, int batch,
+                   void *stream) {
+    mf_model *m = const_cast<mf_model *>(mc);
+    if (!m || batch < 0) return fail(MF_ERR_ARG, "bad argument");
+    int e = check_serial(m);
+    if (e) return e;
+    DevFrame *F;
+    if ((e = frame_dev(m, frame, &F))) return e;
+    if (batch == 0) return MF_OK;
+    hipLaunchKernelGGL(k_bridge_kin<MF_MAX_JOINTS>, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       m->d_model, F, q, pos, rot, J, batch);
+    HIPCHK(hipGetLastError());
+    return MF_OK;
+}
+extern "C" int mf_fk_dev(const mf_model *m, int frame, const double *q, double *pos3, double *rot9, int batch,
+                         void *stream) {
+    return kin_dev(m, frame, q, pos3, rot9, nullptr, batch, stream);
+}
+extern "C" int mf_jac_dev(const mf_model *m, int frame, const double *q, double *J, int batch, void *stream) {
+    return kin_dev(m, frame, q, nullptr, nullptr, J, batch, stream);
+}
+
+// host-pointer wrappers: stage through device buffers
+struct DBuf {
+    double *p = nullptr;
+    ~DBuf() { if (p) (void)hipFree(p); }
+};
+static int dalloc(DBuf &b, size_t n) {
+    HIPCHK(hipMalloc(&b.p, (n ? n : 1) * sizeof(double)));
+    return MF_OK;
+}
+static int h2d(DBuf &b, const double *h, size_t n) {
+    int e = dalloc(b, n);
+    if (e) return e;
+    if (n) HIPCHK(hipMemcpy(b.p, h, n * sizeof(double), hipMemcpyHostToDevice));
+    return MF_OK;
+}
+
+extern "C" int mf_id(const mf_model *m, const double *q, const double *qd, const double *qdd, double *tau, int batch) {
+    if (!m || !q || !qd || !qdd || !tau || batch < 0) return fail(MF_ERR_ARG, "null argument");
+    int e = ensure_device();
+    if (e) return e;
+    size_t n = (size_t)m->host.joints.size() * batch;
+    DBuf a, b, c, t;
+    if ((e = h2d(a, q, n)) || (e = h2d(b, qd, n)) || (e = h2d(c, qdd, n)) || (e = dalloc(t, n))) return e;
+    if ((e = mf_id_dev(m, a.p, b.p, c.p, t.p, batch, nullptr))) return e;
+    HIPCHK(hipMemcpy(tau, t.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    return MF_OK;
+}
+extern "C" int mf_fk(const mf_model *m, int frame, const double *q, double *pos3, double *rot9, int batch) {
+    if (!m || !q || batch < 0) return fail(MF_ERR_ARG, "null argument");
+    int e = ensure_device();
+    if (e) return e;
+    size_t n = (size_t)m->host.joints.size() * batch;
+    DBuf a, p, r;
+    if ((e = h2d(a, q, n)) || (e = dalloc(p, 3 * (size_t)batch)) || (e = dalloc(r, 9 * (size_t)batch))) return e;
+    if ((e = mf_fk_dev(m, frame, a.p, p.p, r.p, batch, nullptr))) return e;
+    if (pos3) HIPCHK(hipMemcpy(pos3, p.p, 3 * (size_t)batch * sizeof(double), hipMemcpyDeviceToHost));
+    if (rot9) HIPCHK(hipMemcpy(rot9, r.p, 9 * (size_t)batch * sizeof(double), hipMemcpyDeviceToHost));
+    return MF_OK;
+}
+extern "C" int mf_jac(const mf_model *m, int frame, const double *q, double *J, int batch) {
+    if (!m || !q || !J || batch < 0) return fail(MF_ERR_ARG, "null argument");
+    int e = ensure_device();
+    if (e) return e;
+    size_t n = (size_t)m->host.joints.size() * batch;
+    DBuf a, j;
+    if ((e = h2d(a, q, n)) || (e = dalloc(j, 6 * n))) return e;
+    if ((e = mf_jac_dev(m, frame, a.p, j.p, batch, nullptr))) return e;
+    HIPCHK(hipMemcpy(J, j.p, 6 * n * sizeof(double), hipMemcpyDeviceToHost));
+    return MF_OK;
+}
+
+// ====================================================================== problems
+struct mf_problem {
+    mf_model *model;
+    mf_problem_spec spec;
+    std::vector<double> tau_lo, tau_hi;
+    OcpConst C;
+    DevFrame *d_frame = nullptr;
+    double *d_tlo = nullptr, *d_thi = nullptr;
+    // solver workspace (grown on demand)
+    int cap = 0;
+    std::vector<double *> bufs;
+    IpmArrays A;
+    ProbState *d_st = nullptr;
+    int *d_active = nullptr;
+};
+
+static void free_ws(mf_problem *p) {
+    for (double *b : p->bufs) (void)hipFree(b);
+    p->bufs.clear();
+    if (p->d_st) (void)hipFree(p->d_st);
+    if (p->d_active) (void)hipFree(p->d_active);
+    p->d_st = nullptr;
+    p->d_active = nullptr;
+    p->cap = 0;
+}
+
+extern "C" int mf_problem_create(const mf_model *mc, const mf_problem_spec *spec, mf_problem **out) {
+    mf_model *m = const_cast<mf_model *>(mc);
+    if (!m || !spec || !out) return fail(MF_ERR_ARG, "null argument");
+    int n = (int)m->host.joints.size();
+    if (spec->N < 1 || spec->h <= 0) return fail(MF_ERR_ARG, "N >= 1 and h > 0 required");
+    if (spec->nf < 0 || spec->nf > 3) return fail(MF_ERR_ARG, "nf must be 0..3");
+    if (spec->frame < 0 || spec->frame >= (int)m->host.frames.size()) return fail(MF_ERR_FRAME, "frame index out of range");
+    if (!spec->tau_lo || !spec->tau_hi) return fail(MF_ERR_ARG, "tau bounds required");
+    int e = check_serial(m);
+    if (e) return e;
+    int nl = spec->use_line ? 2 : 0;
+    if (!((n == 3 && spec->nf == 0 && nl == 0) || (n == 6 && spec->nf == 1 && nl == 2) || (n == 6 && spec->nf == 0 && nl == 0)))
+        return fail(MF_ERR_UNSUPPORTED, "no kernel instantiation for (n, nf, nl) = (" + std::to_string(n) + ", " +
+                                            std::to_string(spec->nf) + ", " + std::to_string(nl) + ")");
+    mf_problem *p = new mf_problem();
+    p->model = m;
+    p->spec = *spec;
+    size_t nb = (size_t)spec->N * n;
+    p->tau_lo.assign(spec->tau_lo, spec->tau_lo + nb);
+    p->tau_hi.assign(spec->tau_hi, spec->tau_hi + nb);
+    p->spec.tau_lo = p->tau_lo.data();
+    p->spec.tau_hi = p->tau_hi.data();
+    OcpConst &C = p->C;
+    memset(&C, 0, sizeof C);
+    C.N = spec->N; C.n = n; C.nf = spec->nf; C.nl = nl;
+    C.nv = 2 * n + spec->nf;
+    C.mb = 3 * n + spec->nf + nl;
+    C.npair = C.nv * (C.nv + 1) / 2;
+    C.h = spec->h;
+    memcpy(C.fdir, spec->fdir, sizeof C.fdir);
+    C.wF = spec->wF; C.wqd = spec->wqd; C.wtau = spec->wtau;
+    memcpy(C.qd0, spec->qd0, sizeof C.qd0);
+    memcpy(C.qd_lo, spec->qd_lo, sizeof C.qd_lo);
+    memcpy(C.qd_hi, spec->qd_hi, sizeof C.qd_hi);
+    memcpy(C.q_lo, spec->q_lo, sizeof C.q_lo);
+    memcpy(C.q_hi, spec->q_hi, sizeof C.q_hi);
+    *out = p;
+    return MF_OK;
+}
+
+extern "C" void mf_problem_free(mf_problem *p) {
+    if (!p) return;
+    free_ws(p);
+    if (p->d_tlo) (void)hipFree(p->d_tlo);
+    if (p->d_thi) (void)hipFree(p->d_thi);
+    delete p;
+}
+
+extern "C" int mf_problem_wsize(const mf_problem *p) {
+    if (!p) return fail(MF_ERR_ARG, "null problem");
+    return p->C.n + p->C.N * (2 * p->C.n + p->C.nf);
+}
+
+static int ensure_ws(mf_problem *p, int batch) {
+    int e = upload_model(p->model);
+    if (e) return e;
+    if (!p->d_frame && (e = frame_dev(p->model, p->spec.frame, &p->d_frame))) return e;
+    const OcpConst &C = p->C;
+    size_t nb = (size_t)C.N * C.n;
+    if (!p->d_tlo) {
+        HIPCHK(hipMalloc(&p->d_tlo, nb * sizeof(double)));
+        HIPCHK(hipMalloc(&p->d_thi, nb * sizeof(double)));
+        HIPCHK(hipMemcpy(p->d_tlo, p->tau_lo.data(), nb * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(p->d_thi, p->tau_hi.data(), nb * sizeof(double), hipMemcpyHostToDevice));
+    }
+    if (p->cap >= batch) return MF_OK;
+    free_ws(p);
+    IpmSizes S = ipm_sizes(C);
+    IpmArrays &A = p->A;
+    struct Item { double **ptr; size_t n; };
+    Item items[] = {
+        {&A.q, S.q}, {&A.qd, S.u}, {&A.F, S.f}, {&A.s, S.u}, {&A.yc, S.u}, {&A.yl, S.l}, {&A.yd, S.u},
+        {&A.zqL, S.q}, {&A.zqU, S.q}, {&A.zdL, S.u}, {&A.zdU, S.u}, {&A.vL, S.u}, {&A.vU, S.u},
+        {&A.dq, S.q}, {&A.dqd, S.u}, {&A.dF, S.f}, {&A.ds, S.u}, {&A.dyc, S.u}, {&A.dyl, S.l}, {&A.dyd, S.u},
+        {&A.dzqL, S.q}, {&A.dzqU, S.q}, {&A.dzdL, S.u}, {&A.dzdU, S.u}, {&A.dvL, S.u}, {&A.dvU, S.u},
+        {&A.tau, S.u}, {&A.Jt, S.jt}, {&A.line, S.l}, {&A.Jl, S.jl}, {&A.W, S.w}, {&A.gf, S.gf}, {&A.cost, S.cost},
+        {&A.Sxq, S.q}, {&A.gphq, S.q}, {&A.Sxd, S.u}, {&A.gphd, S.u}, {&A.Ss, S.u}, {&A.gphs, S.u},
+        {&A.G, S.G}, {&A.wv, S.wv}, {&A.q0, (size_t)C.n}, {&A.lref, 2},
+    };
+    for (auto &it : items) {
+        double *ptr = nullptr;
+        hipError_t he = hipMalloc(&ptr, it.n * (size_t)batch * sizeof(double));
+        if (he != hipSuccess) {
+            free_ws(p);
+            return fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
+        }
+        (void)hipMemset(ptr, 0, it.n * (size_t)batch * sizeof(double));
+        p->bufs.push_back(ptr);
+        *it.ptr = ptr;
+    }
+    HIPCHK(hipMalloc(&p->d_st, sizeof(ProbState) * (size_t)batch));
+    HIPCHK(hipMalloc(&p->d_active, sizeof(int)));
+    A.st = p->d_st;
+    A.active = p->d_active;
+    A.tau_lo = p->d_tlo;
+    A.tau_hi = p->d_thi;
+    p->cap = batch;
+    return MF_OK;
+}
+
+static int solve_core(mf_problem *p, int batch, const double *d_q0, const double *d_lref, const mf_solver_opts *o,
+                      double *d_w, int *d_status, int *d_iters, double *d_kkt, double *d_obj, hipStream_t s) {
+    int e = ensure_ws(p, batch);
+    if (e) return e;
+    OcpConst C = p->C;
+    C.tol = o ? o->tol : 1e-8;
+    C.constr_viol_tol = o ? o->constr_viol_tol : 1e-8;
+    C.max_iter = o ? o->max_iter : 200;
+    C.mu_init = o ? o->mu_init : 0.1;
+    C.F_init = o ? o->F_init : 0.0;
+    IpmArrays A = p->A;
+    const int n = C.n;
+    HIPCHK(hipMemcpyAsync(A.q0, d_q0, sizeof(double) * n * (size_t)batch, hipMemcpyDeviceToDevice, s));
+    if (d_lref) {
+        HIPCHK(hipMemcpyAsync(A.lref, d_lref, sizeof(double) * 2 * (size_t)batch, hipMemcpyDeviceToDevice, s));
+    } else {
+        std::vector<double> lr(2 * (size_t)batch);
+        for (int b = 0; b < batch; b++) { lr[2 * b] = p->spec.line_ref[0]; lr[2 * b + 1] = p->spec.line_ref[1]; }
+        HIPCHK(hipMemcpyAsync(A.lref, lr.data(), sizeof(double) * lr.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    HIPCHK(hipMemcpyAsync(A.active, &batch, sizeof(int), hipMemcpyHostToDevice, s));
+    DevFrame *F = p->d_frame;
+    if (!ipm_dispatch(n, C.nf, C.nl, 0, p->model->d_model, F, C, A, batch, s, nullptr, nullptr, nullptr, nullptr, nullptr))
+        return fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
+    HIPCHK(hipGetLastError());
+    int active = batch;
+    const int chunk = 4;
+    for (int it = 0; it <= C.max_iter && active > 0; it += chunk) {
+        for (int c = 0; c < chunk; c++)
+            ipm_dispatch(n, C.nf, C.nl, 1, p->model->d_model, F, C, A, batch, s, nullptr, nullptr, nullptr, nullptr, nullptr);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (o && o->verbose) fprintf(stderr, "[mf] after %d iterations: %d running\n", it + chunk, active);
+    }
+    ipm_dispatch(n, C.nf, C.nl, 2, p->model->d_model, F, C, A, batch, s, d_w, d_status, d_iters, d_kkt, d_obj);
+    HIPCHK(hipGetLastError());
+    return MF_OK;
+}
+
+extern "C" int mf_solve_batch_dev(mf_problem *p, int batch, const double *q0, const double *line_ref,
+                                  const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt,
+                                  double *obj, void *stream) {
+    if (!p || !q0 || !w || batch < 1) return fail(MF_ERR_ARG, "bad argument");
+    int e = ensure_device();
+    if (e) return e;
+    return solve_core(p, batch, q0, line_ref, opts, w, status, iters, kkt, obj, (hipStream_t)stream);
+}
+
+extern "C" int mf_solve_batch(mf_problem *p, int batch, const double *q0, const double *line_ref,
+                              const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt, double *obj,
+                              int device) {
+    if (!p || !q0 || !w || batch < 1) return fail(MF_ERR_ARG, "bad argument");
+    int e = ensure_device();
+    if (e) return e;
+    HIPCHK(hipSetDevice(device));
+    const int n = p->C.n, ws = mf_problem_wsize(p);
+    DBuf dq0, dl, dw, dk, dob;
+    int *dst = nullptr, *dit = nullptr;
+    if ((e = h2d(dq0, q0, (size_t)n * batch))) return e;
+    if (line_ref && (e = h2d(dl, line_ref, 2 * (size_t)batch))) return e;
+    if ((e = dalloc(dw, (size_t)ws * batch)) || (e = dalloc(dk, batch)) || (e = dalloc(dob, batch))) return e;
+    HIPCHK(hipMalloc(&dst, sizeof(int) * batch));
+    HIPCHK(hipMalloc(&dit, sizeof(int) * batch));
+    e = solve_core(p, batch, dq0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst, dit, dk.p, dob.p, nullptr);
+    if (!e) {
+        hipError_t he = hipDeviceSynchronize();
+        if (he != hipSuccess) e = fail(MF_ERR_DEVICE, hipGetErrorString(he));
+    }
+    if (!e) {
+        (void)hipMemcpy(w, dw.p, sizeof(double) * ws * (size_t)batch, hipMemcpyDeviceToHost);
+        if (status) (void)hipMemcpy(status, dst, sizeof(int) * batch, hipMemcpyDeviceToHost);
+        if (iters) (void)hipMemcpy(iters, dit, sizeof(int) * batch, hipMemcpyDeviceToHost);
+        if (kkt) (void)hipMemcpy(kkt, dk.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
+        if (obj) (void)hipMemcpy(obj, dob.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(dst);
+    (void)hipFree(dit);
+    return e;
+}
+
+// ====================================================================== node evaluation
+template <int NJ, int NF>
+__global__ __launch_bounds__(256) void k_node_eval(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                                   OcpConst C, const double *x, const double *uu, const double *lref,
+                                                   double dl0, double dl1, double *xnext, double *g, double *cost,
+                                                   double *jac, int nodes) {
+    __shared__ DevModel M;
+    __shared__ DevFrame F;
+    {
+        const double *s = reinterpret_cast<const double *>(Mg);
+        double *d = reinterpret_cast<double *>(&M);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevModel) / sizeof(double)); i += blockDim.x) d[i] = s[i];
+        const double *s2 = reinterpret_cast<const double *>(Fg);
+        double *d2 = reinterpret_cast<double *>(&F);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevFrame) / sizeof(double)); i += blockDim.x) d2[i] = s2[i];
+    }
+    __syncthreads();
+    constexpr int NV = 2 * NJ + NF;
+    constexpr int NFA = NF > 0 ? NF : 1;
+    long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= (long)nodes * NV) return;
+    const int col = (int)(t % NV);
+    const int r = (int)(t / NV);
+    const int nl = C.nl, nrow = 2 * NJ + nl + 1;
+    const double *q = x + (size_t)r * NJ, *u = uu + (size_t)r * (NJ + NF);
+    Dual xq[NJ], xqd[NJ], xF[NFA], tau[NJ], pf[3];
+    for (int i = 0; i < NJ; i++) {
+        xq[i] = Dual(q[i], col == i ? 1.0 : 0.0);
+        xqd[i] = Dual(u[i], col == NJ + i ? 1.0 : 0.0);
+    }
+    for (int a = 0; a < NFA; a++) xF[a] = Dual(NF > 0 ? u[NJ + a] : 0.0, col == 2 * NJ + a ? 1.0 : 0.0);
+    node_tau<Dual, NJ>(M, F, NF, C.fdir, xq, xqd, xF, tau, pf);
+    Dual c(0.0);
+    for (int a = 0; a < NF; a++) c += xF[a] * xF[a] * C.wF;
+    for (int j = 0; j < NJ; j++) c += xqd[j] * xqd[j] * C.wqd + tau[j] * tau[j] * C.wtau;
+    double *J = jac + (size_t)r * nrow * NV + (size_t)col * nrow;  // column-major per node
+    for (int j = 0; j < NJ; j++) J[j] = (col == j ? 1.0 : 0.0) + (col == NJ + j ? C.h : 0.0);
+    for (int j = 0; j < NJ; j++) J[NJ + j] = tau[j].d;
+    for (int l = 0; l < nl; l++) J[2 * NJ + l] = pf[l].d;
+    J[2 * NJ + nl] = c.d;
+    if (col == 0) {
+        for (int j = 0; j < NJ; j++) xnext[(size_t)r * NJ + j] = q[j] + C.h * u[j];
+        for (int j = 0; j < NJ; j++) g[(size_t)r * (NJ + nl) + j] = tau[j].v;
+        for (int l = 0; l < nl; l++) {
+            double ref = lref ? lref[(size_t)r * 2 + l] : (l == 0 ? dl0 : dl1);
+            g[(size_t)r * (NJ + nl) + NJ + l] = pf[l].v - ref;
+        }
+        cost[r] = c.v;
+    }
+}
+
+extern "C" int mf_node_eval(const mf_problem *pc, const double *x, const double *u, const double *line_ref,
+                            double *xnext, double *g, double *cost, double *jac, int nodes) {
+    mf_problem *p = const_cast<mf_problem *>(pc);
+    if (!p || !x || !u || !xnext || !g || !cost || !jac || nodes < 0) return fail(MF_ERR_ARG, "null argument");
+    int e = ensure_device();
+    if (e) return e;
+    if ((e = upload_model(p->model))) return e;
+    if (!p->d_frame && (e = frame_dev(p->model, p->spec.frame, &p->d_frame))) return e;
+    if (nodes == 0) return MF_OK;
+    const OcpConst &C = p->C;
+    const int n = C.n, nf = C.nf, nl = C.nl, nv = C.nv, nrow = 2 * n + nl + 1;
+    DBuf dx, du, dl, dxn, dg, dc, dj;
+    if ((e = h2d(dx, x, (size_t)n * nodes)) || (e = h2d(du, u, (size_t)(n + nf) * nodes))) return e;
+    if (line_ref && (e = h2d(dl, line_ref, 2 * (size_t)nodes))) return e;
+    if ((e = dalloc(dxn, (size_t)n * nodes)) || (e = dalloc(dg, (size_t)(n + nl) * nodes)) || (e = dalloc(dc, nodes)) ||
+        (e = dalloc(dj, (size_t)nrow * nv * nodes)))
+        return e;
+    long total = (long)nodes * nv;
+    dim3 grid((unsigned)((total + 255) / 256)), blk(256);
+    const double *lr = line_ref ? dl.p : nullptr;
+    if (n == 6 && nf == 1)
+        hipLaunchKernelGGL((k_node_eval<6, 1>), grid, blk, 0, 0, p->model->d_model, p->d_frame, C, dx.p, du.p, lr,
+                           p->spec.line_ref[0], p->spec.line_ref[1], dxn.p, dg.p, dc.p, dj.p, nodes);
+    else if (n == 6 && nf == 0)
+        hipLaunchKernelGGL((k_node_eval<6, 0>), grid, blk, 0, 0, p->model->d_model, p->d_frame, C, dx.p, du.p, lr,
+                           p->spec.line_ref[0], p->spec.line_ref[1], dxn.p, dg.p, dc.p, dj.p, nodes);
+    else if (n == 3 && nf == 0)
+        hipLaunchKernelGGL((k_node_eval<3, 0>), grid, blk, 0, 0, p->model->d_model, p->d_frame, C, dx.p, du.p, lr,
+                           p->spec.line_ref[0], p->spec.line_ref[1], dxn.p, dg.p, dc.p, dj.p, nodes);
+    else
+        return fail(MF_ERR_UNSUPPORTED, "no node-eval instantiation for this problem");
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(xnext, dxn.p, sizeof(double) * n * (size_t)nodes, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(g, dg.p, sizeof(double) * (n + nl) * (size_t)nodes, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cost, dc.p, sizeof(double) * (size_t)nodes, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(jac, dj.p, sizeof(double) * nrow * nv * (size_t)nodes, hipMemcpyDeviceToHost));
+    return MF_OK;
+}

@@ -55,17 +55,28 @@ def pilz6_q0() -> np.ndarray:
         return np.array(json.load(f)["q0"], float)
 
 
-def pilz6_force(N: int = 100, T: float = 2.0, q0=None, line_ref=(0.1, 0.4)) -> dict:
+# The reference's fatigue floor (bound_torque = 15 Nm, force_optimization_pilz_6DOF.py:89)
+# makes the Pilz-6DOF force problem infeasible: over every configuration with
+# prbt_link_5 on the line x=0.1, y=0.4 the smallest achievable max joint torque
+# (gravity, best x-force) is 16.64 Nm (tests/test_problems.py reproduces it).
+# The benchmark instance keeps every other constant and uses the smallest round
+# floor that is feasible from the IK start, 30 Nm.
+REFERENCE_FLOOR = 15.0
+BENCH_FLOOR = 30.0
+BENCH_F_INIT = 1.0   # IPOPT's x0 = 0 starts on the F = 0 saddle of -F^2
+
+
+def pilz6_force(N: int = 100, T: float = 2.0, q0=None, line_ref=(0.1, 0.4), tau_floor: float = REFERENCE_FLOOR) -> dict:
     """C2: ``python/Pilz_6_DOF/force_optimization_pilz_6DOF.py`` at N shooting nodes.
 
     T=2 (L78), tau0=50, alpha=2, qd in +-0.4, bound 15 (L84-89), line on
     prbt_link_5 x/y (L150-156), cost -F^T F with F = [Fx,0,0,0,0,0] (L131-134, L177).
     """
     h = T / N
-    B = torque_envelope(N, h, 50.0, 2.0, 15.0)
+    B = torque_envelope(N, h, 50.0, 2.0, tau_floor)
     n = 6
     return dict(
-        name="pilz6_force", urdf="pilz_robot_6DOF.urdf", frame="prbt_link_5",
+        name="pilz6_force", urdf="pilz_robot_6DOF.urdf", frame="prbt_link_5", tau_floor=tau_floor,
         N=N, h=h, nf=1, fdir=[[1.0, 0.0, 0.0]],
         use_line=True, line_ref=list(line_ref),
         wF=-1.0, wqd=0.0, wtau=0.0,
@@ -102,3 +113,8 @@ def pilz6_batch_q0(batch: int, seed: int = 0, spread: float = 0.05, q0=None) -> 
     base = pilz6_q0() if q0 is None else np.asarray(q0, float)
     rng = np.random.default_rng(seed)
     return base[None, :] + rng.uniform(-spread, spread, size=(batch, base.size))
+
+
+def pilz6_bench(N: int = 100, q0=None, line_ref=(0.1, 0.4)) -> dict:
+    """The benchmark instance of C2 (feasible fatigue floor, see BENCH_FLOOR)."""
+    return pilz6_force(N=N, q0=q0, line_ref=line_ref, tau_floor=BENCH_FLOOR)
