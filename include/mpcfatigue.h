@@ -126,6 +126,12 @@ int mf_solve_batch_dev(mf_problem *p, int batch, const double *q0, const double 
                        const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt, double *obj,
                        void *stream);
 
+/* Per-kernel device time of the solver's launches on the solve stream (HIP events):
+ * index 0 = node values + Jacobians (k_eval_jac), 1 = Lagrangian Hessians
+ * (k_eval_hess), 2 = per-problem IPM step (k_ipm_iter).  Enabling resets the totals. */
+int mf_problem_timing(mf_problem *p, int enable);
+int mf_problem_kernel_stats(const mf_problem *p, double *ms_total3, long *launches3);
+
 const char *mf_last_error(void);
 
 #ifdef __cplusplus

@@ -50,9 +50,9 @@ struct BKInertia {
     int pos, neg, zero;
 };
 
-// c0, c1: LDS scratch of length >= m.  perm/piv: LDS int arrays of length >= m.
+// perm/piv: LDS int arrays of length >= m.
 template <int LD>
-__device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv, double *c0, double *c1) {
+__device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
     const int lane = threadIdx.x;
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     BKInertia in{0, 0, 0};
@@ -91,6 +91,7 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv, doubl
         }
         int kk = k + kstep - 1;
         if (kp != kk) {
+            __syncthreads();  // previous pivot's L-column writes must land before rows move
             for (int j = lane; j < m; j += 64) {
                 double t = A[kk * LD + j]; A[kk * LD + j] = A[kp * LD + j]; A[kp * LD + j] = t;
             }
@@ -105,25 +106,24 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv, doubl
             double d = A[k * LD + k];
             if (d > 0) in.pos++; else if (d < 0) in.neg++; else in.zero++;
             double inv = 1.0 / d;
-            for (int i = k + 1 + lane; i < m; i += 64) c0[i] = A[i * LD + k];
-            __syncthreads();
+            // trailing update reads the (unmodified) pivot column directly
             int t = m - k - 1;
             for (int e = lane; e < t * t; e += 64) {
                 int i = k + 1 + e / t, j = k + 1 + e % t;
                 if (j <= i) {
-                    double val = A[i * LD + j] - (c0[i] * inv) * c0[j];
+                    double ci = A[i * LD + k], cj = A[j * LD + k];
+                    double val = A[i * LD + j] - (ci * inv) * cj;
                     A[i * LD + j] = val;
                     A[j * LD + i] = val;
                 }
             }
             __syncthreads();
             for (int i = k + 1 + lane; i < m; i += 64) {
-                double l = c0[i] * inv;
+                double l = A[i * LD + k] * inv;
                 A[i * LD + k] = l;
                 A[k * LD + i] = l;
             }
             if (lane == 0) piv[k] = 1;
-            __syncthreads();
         } else {
             double a = A[k * LD + k], b = A[(k + 1) * LD + k], c = A[(k + 1) * LD + k + 1];
             double det = a * c - b * b;
@@ -131,26 +131,26 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv, doubl
             else if (det > 0) { if (a + c > 0) in.pos += 2; else in.neg += 2; }
             else in.zero += 2;
             double ia = c / det, ib = -b / det, ic = a / det;
-            for (int i = k + 2 + lane; i < m; i += 64) { c0[i] = A[i * LD + k]; c1[i] = A[i * LD + k + 1]; }
-            __syncthreads();
             int t = m - k - 2;
             for (int e = lane; e < t * t; e += 64) {
                 int i = k + 2 + e / t, j = k + 2 + e % t;
                 if (j <= i) {
-                    double l0 = c0[i] * ia + c1[i] * ib, l1 = c0[i] * ib + c1[i] * ic;
-                    double val = A[i * LD + j] - (l0 * c0[j] + l1 * c1[j]);
+                    double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
+                    double c0j = A[j * LD + k], c1j = A[j * LD + k + 1];
+                    double l0 = c0i * ia + c1i * ib, l1 = c0i * ib + c1i * ic;
+                    double val = A[i * LD + j] - (l0 * c0j + l1 * c1j);
                     A[i * LD + j] = val;
                     A[j * LD + i] = val;
                 }
             }
             __syncthreads();
             for (int i = k + 2 + lane; i < m; i += 64) {
-                double l0 = c0[i] * ia + c1[i] * ib, l1 = c0[i] * ib + c1[i] * ic;
+                double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
+                double l0 = c0i * ia + c1i * ib, l1 = c0i * ib + c1i * ic;
                 A[i * LD + k] = l0;
                 A[i * LD + k + 1] = l1;
             }
             if (lane == 0) { piv[k] = 2; piv[k + 1] = 0; }
-            __syncthreads();
         }
         k += kstep;
     }

@@ -354,6 +354,11 @@ struct mf_problem {
     OcpConst C;
     DevFrame *d_frame = nullptr;
     double *d_tlo = nullptr, *d_thi = nullptr;
+    // per-kernel timing (HIP events on the solve stream), enabled by mf_problem_timing
+    int timing = 0;
+    std::vector<hipEvent_t> ev;
+    double t_ms[3] = {0, 0, 0};
+    long t_launch[3] = {0, 0, 0};
     // solver workspace (grown on demand)
     int cap = 0;
     std::vector<double *> bufs;
@@ -415,6 +420,7 @@ extern "C" int mf_problem_create(const mf_model *mc, const mf_problem_spec *spec
 extern "C" void mf_problem_free(mf_problem *p) {
     if (!p) return;
     free_ws(p);
+    for (auto e : p->ev) (void)hipEventDestroy(e);
     if (p->d_tlo) (void)hipFree(p->d_tlo);
     if (p->d_thi) (void)hipFree(p->d_thi);
     delete p;
@@ -500,12 +506,30 @@ static int solve_core(mf_problem *p, int batch, const double *d_q0, const double
     HIPCHK(hipGetLastError());
     int active = batch;
     const int chunk = 4;
+    if (p->timing && p->ev.size() < (size_t)(6 * chunk)) {
+        for (auto e2 : p->ev) (void)hipEventDestroy(e2);
+        p->ev.assign(6 * chunk, nullptr);
+        for (auto &e2 : p->ev) HIPCHK(hipEventCreate(&e2));
+    }
     for (int it = 0; it <= C.max_iter && active > 0; it += chunk) {
         for (int c = 0; c < chunk; c++)
-            ipm_dispatch(n, C.nf, C.nl, 1, p->model->d_model, F, C, A, batch, s, nullptr, nullptr, nullptr, nullptr, nullptr);
+            for (int ph = 0; ph < 3; ph++) {
+                if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * 3 + ph) * 2], s));
+                ipm_dispatch(n, C.nf, C.nl, 10 + ph, p->model->d_model, F, C, A, batch, s, nullptr, nullptr, nullptr,
+                             nullptr, nullptr);
+                if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * 3 + ph) * 2 + 1], s));
+            }
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        if (p->timing)
+            for (int c = 0; c < chunk; c++)
+                for (int ph = 0; ph < 3; ph++) {
+                    float ms = 0;
+                    HIPCHK(hipEventElapsedTime(&ms, p->ev[(c * 3 + ph) * 2], p->ev[(c * 3 + ph) * 2 + 1]));
+                    p->t_ms[ph] += ms;
+                    p->t_launch[ph]++;
+                }
         if (o && o->verbose) fprintf(stderr, "[mf] after %d iterations: %d running\n", it + chunk, active);
     }
     ipm_dispatch(n, C.nf, C.nl, 2, p->model->d_model, F, C, A, batch, s, d_w, d_status, d_iters, d_kkt, d_obj);
@@ -642,5 +666,18 @@ extern "C" int mf_node_eval(const mf_problem *pc, const double *x, const double 
     HIPCHK(hipMemcpy(g, dg.p, sizeof(double) * (n + nl) * (size_t)nodes, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(cost, dc.p, sizeof(double) * (size_t)nodes, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(jac, dj.p, sizeof(double) * nrow * nv * (size_t)nodes, hipMemcpyDeviceToHost));
+    return MF_OK;
+}
+
+extern "C" int mf_problem_timing(mf_problem *p, int enable) {
+    if (!p) return fail(MF_ERR_ARG, "null problem");
+    p->timing = enable ? 1 : 0;
+    for (int k = 0; k < 3; k++) { p->t_ms[k] = 0; p->t_launch[k] = 0; }
+    return MF_OK;
+}
+
+extern "C" int mf_problem_kernel_stats(const mf_problem *p, double *ms_total3, long *launches3) {
+    if (!p || !ms_total3 || !launches3) return fail(MF_ERR_ARG, "null argument");
+    for (int k = 0; k < 3; k++) { ms_total3[k] = p->t_ms[k]; launches3[k] = p->t_launch[k]; }
     return MF_OK;
 }

@@ -24,6 +24,24 @@ namespace mf {
 
 __device__ __forceinline__ bool hasb(double b) { return isfinite(b); }
 
+// Diagnostic build only (-DMF_PHASE_STAMPS): per-phase cycle counts of k_ipm_iter,
+// accumulated by lane 0 into a debug buffer (never read by the solver).
+#ifdef MF_PHASE_STAMPS
+__device__ unsigned long long mf_stamp_buf[16 * 4096];
+#define STAMP(slot)                                                                   \
+    do {                                                                              \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
+        if (lane == 0 && b < 4096) mf_stamp_buf[b * 16 + (slot)] += t_ - t_prev_;     \
+        t_prev_ = t_;                                                                 \
+    } while (0)
+#define STAMP_INIT unsigned long long t_prev_ = __builtin_amdgcn_s_memtime()
+#define STAMP_COUNT(slot, v) do { if (lane == 0 && b < 4096) mf_stamp_buf[b * 16 + (slot)] += (v); } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#define STAMP_INIT do {} while (0)
+#define STAMP_COUNT(slot, v) do {} while (0)
+#endif
+
 // cooperative copy of a POD struct into LDS
 template <class T> __device__ __forceinline__ void stage_lds(T *dst, const T *src) {
     const int words = (int)(sizeof(T) / sizeof(double));
@@ -220,7 +238,7 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
     }
     if (lane == 0) {
         ProbState st;
-        st.mu = C.mu_init; st.nu = 0.0; st.dw_last = 0.0; st.dF_last = 0.0;
+        st.mu = C.mu_init; st.nu = 0.0; st.reg_last = 0.0; st.reg_tier = 0;
         st.E0 = INFINITY; st.cviol = INFINITY; st.obj = 0.0;
         st.status = ST_RUNNING; st.iter = 0; st.n_ls_fail = 0; st.n_ic = 0; st.consec_fail = 0;
         A.st[b] = st;
@@ -236,14 +254,8 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     constexpr int NFA = NF > 0 ? NF : 1;
     constexpr int NLA = NL > 0 ? NL : 1;
     constexpr int MB = 3 * NJ + NF + NL;
-    constexpr int LD = MB + 1;
-    constexpr int NR = NJ + 1;
-    constexpr int oyc = 0, oq = NJ, oqd = 2 * NJ, oF = 3 * NJ, oyl = 3 * NJ + NF;
     __shared__ DevModel M;
     __shared__ DevFrame F;
-    __shared__ double Dm[MB * LD];
-    __shared__ double RH[MB * NR], Yb[MB * NR];
-    __shared__ double c0[MB], c1[MB], ybuf[MB], ynext[MB];
     __shared__ double Dd_s[NJ], rdd_s[NJ];
     __shared__ int perm[MB], piv[MB];
     const int b = blockIdx.x, lane = threadIdx.x;
@@ -253,6 +265,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     stage_lds(&M, Mg);
     stage_lds(&F, Fg);
     __syncthreads();
+    STAMP_INIT;
 
     const IpmSizes S = ipm_sizes(C);
     const int N = C.N;
@@ -381,6 +394,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
     }
     const double tau_fb = fmax(tau_min, 1.0 - mu);
+    STAMP(0);
 
     // ---------------- barrier Sigma and gradients
     for (int e = lane; e < (N + 1) * n; e += 64) {
@@ -409,160 +423,237 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     __threadfence_block();
     __syncthreads();
 
-    // ---------------- inertia-corrected block LDL^T
+    STAMP(1);
+    // ---------------- inertia-corrected Riccati recursion
+    // Stage k (1 <= k < N): x = dq_k (n), u = (dqd_k, dF_k) (NU), dynamics dx_{k+1} = dx_k + B du_k + c_k
+    // with B = [h I, 0].  The line constraint of stage k+1 is pushed back onto stage k:
+    // Jl_{k+1} (dx_k + B du_k + c_k) + line_{k+1} = 0.  Per stage the (NU+NL) block
+    // [[Quu, Du^T], [Du, -dc]] is factorised by Bunch-Kaufman; the KKT matrix has the inertia
+    // (n_primal, n_dual) iff every stage block has inertia (NU, NL) (Sylvester),
+    // which is the test the oracle's block LDL^T of the whole KKT performs.  Stage 0 has x, qd
+    // fixed: only dF_0 with Hessian H_FF.  Slot k of G / wv keeps Ku, Kl, P_{k+1} / ku, kl, p_{k+1}.
+    constexpr int NU = NJ + NF;
+    constexpr int NK = NU + NL;
+    constexpr int LDK = NK + 1;
+    constexpr int NRK = NJ + 1;
+    constexpr int NLA2 = NL > 0 ? NL : 1;
+    __shared__ double Hs[NV * NV], gs[NV];
+    __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], cs[NJ], Pn[NJ * NJ];
+    __shared__ double Ks[NK * LDK], Rk[NK * NRK], Yk[NK * NRK];
+    __shared__ double Gl[NLA2 * NJ], el[NLA2];
+    __shared__ double xs[NJ], us[NU + NLA2];
     double dw = 0.0, dc = 0.0, dFr = 0.0;
-    const double dw_last0 = st.dw_last, dF_last0 = st.dF_last;
-    int tier = (nf > 0 && C.wF < 0) ? 1 : 2;
+    const int reg_tier0 = st.reg_tier;
+    const double reg_last0 = st.reg_last;
+    int tier = reg_tier0, step_no = 0;
+    double reg = (reg_tier0 == 0) ? 0.0 : reg_last0 / 3.0;
+    if (reg_tier0 != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
+    if (tier == 1) dFr = reg; else if (tier == 2) dw = reg;
     bool factor_ok = false;
+    int ntries = 0;
     for (int tries = 0; tries < 60; tries++) {
-        int npos = 0, nneg = 0, nzero = 0;
-        for (int k = 0; k <= N; k++) {
-            const int m = (k < N) ? MB : 2 * n;
-            if (k < N) {
-                for (int j = lane; j < n; j += 64) {
-                    int i = k * n + j;
-                    if (TACT(k, j)) {
-                        double sg = Ss[i] + dw;
-                        Dd_s[j] = sg / (1.0 + dc * sg);
-                        rdd_s[j] = (tau[i] - s[i]) + (gphs[i] - yd[i]) / sg;
-                    } else { Dd_s[j] = 0.0; rdd_s[j] = 0.0; }
+        ntries++;
+        bool ok = true, zero = false;
+        // terminal value function V_N = 1/2 x^T P x + p^T x
+        for (int e = lane; e < n * n; e += 64) {
+            int i = e / n, j = e % n;
+            Ps[e] = (i == j) ? Sxq[N * n + i] + dw : 0.0;
+        }
+        for (int j = lane; j < n; j += 64) ps[j] = gphq[N * n + j] - yc[(N - 1) * n + j];
+        __syncthreads();
+        for (int k = N - 1; k >= 0; k--) {
+            const double *Wk = W + (size_t)k * NV * NV, *Jtk = Jt + (size_t)k * n * NV;
+            // ---- stage Hessian H (NV x NV) and gradient g, exactly the primal rows of the KKT
+            for (int j = lane; j < n; j += 64) {
+                int i = k * n + j;
+                if (TACT(k, j)) {
+                    double sg = Ss[i] + dw;
+                    Dd_s[j] = sg / (1.0 + dc * sg);
+                    rdd_s[j] = (tau[i] - s[i]) + (gphs[i] - yd[i]) / sg;
+                } else { Dd_s[j] = 0.0; rdd_s[j] = 0.0; }
+                cs[j] = q[k * n + j] + h * qd[k * n + j] - q[(k + 1) * n + j];
+            }
+            __syncthreads();
+            for (int e = lane; e < NV * NV; e += 64) {
+                int u = e / NV, v = e % NV;
+                double a = Wk[u * NV + v];
+                for (int jj = 0; jj < n; jj++) a += Jtk[jj * NV + u] * Dd_s[jj] * Jtk[jj * NV + v];
+                if (u == v) {
+                    a += dw + (u >= 2 * n ? dFr : 0.0);
+                    if (u < n) a += Sxq[k * n + u];
+                    else if (u < 2 * n) a += Sxd[k * n + u - n];
+                }
+                Hs[e] = a;
+            }
+            for (int u = lane; u < NV; u += 64) {
+                double g = gf[k * NV + u];
+                for (int jj = 0; jj < n; jj++) g += Jtk[jj * NV + u] * (yd[k * n + jj] + Dd_s[jj] * rdd_s[jj]);
+                if (u < n) {
+                    g += gphq[k * n + u] + yc[k * n + u] - (k > 0 ? yc[(k - 1) * n + u] : 0.0);
+                    for (int l = 0; l < nl; l++) g += Jl[(k * nl + l) * n + u] * yl[k * nl + l];
+                } else if (u < 2 * n) {
+                    g += gphd[k * n + u - n] + h * yc[k * n + u - n];
+                }
+                gs[u] = g;
+            }
+            // s = P c + p ; keep P_{k+1}, p_{k+1} for the forward sweep
+            double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
+            for (int j = lane; j < n; j += 64) {
+                double a = ps[j];
+                for (int i = 0; i < n; i++) a += Ps[j * n + i] * cs[i];
+                ss[j] = a;
+                wk[NU + NL + j] = ps[j];
+            }
+            for (int e = lane; e < n * n; e += 64) Gk[(NU + NL) * n + e] = Ps[e];
+            __syncthreads();
+            if (k == 0) {
+                // only dF_0 is free (q_0, qd_0 fixed; the stage-1 line constraint is masked)
+                if (nf > 0) {
+                    for (int e = lane; e < nf * nf; e += 64) Ks[(e / nf) * LDK + e % nf] = Hs[(2 * n + e / nf) * NV + 2 * n + e % nf];
+                    for (int a = lane; a < nf; a += 64) Rk[a * NRK] = -gs[2 * n + a];
+                    __syncthreads();
+                    BKInertia in = bk_factor_wave<LDK>(Ks, nf, perm, piv);
+                    if (in.zero) { ok = false; zero = true; break; }
+                    if (in.pos != nf) { ok = false; break; }
+                    bk_solve_wave<LDK, NRK>(Ks, nf, perm, piv, Rk, 1, Yk);
+                    for (int a = lane; a < nf; a += 64) wk[NJ + a] = Rk[a * NRK];  // dF_0 (ku slot)
+                }
+                __syncthreads();
+                break;
+            }
+            const bool con = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
+            if (con) {
+                const double *Jl1 = Jl + (size_t)(k + 1) * nl * n;
+                for (int e = lane; e < nl * n; e += 64) Gl[e] = Jl1[e];
+                for (int l = lane; l < nl; l += 64) {
+                    double a = line[(k + 1) * nl + l];
+                    for (int i = 0; i < n; i++) a += Jl1[l * n + i] * cs[i];
+                    el[l] = a;
                 }
                 __syncthreads();
             }
-            const double *Wk = W + (size_t)k * NV * NV, *Jtk = Jt + (size_t)k * n * NV, *Jlk = Jl + (size_t)k * nl * n;
-            const double *Gp = G + (size_t)(k > 0 ? k - 1 : 0) * MB * n, *wp = wv + (size_t)(k > 0 ? k - 1 : 0) * MB;
-            auto masked = [&](int i) -> int {  // 1: fixed primal, -1: masked dual, 0: active
-                if (k == 0 && i >= oq && i < oF) return 1;
-                if (k < N && !LINE_ON(k) && i >= oyl && i < oyl + nl) return -1;
-                return 0;
-            };
-            for (int e = lane; e < m * m; e += 64) {
-                int i = e / m, j = e % m;
-                double val = 0.0;
-                int mi = masked(i), mj = masked(j);
-                if (mi || mj) {
-                    val = (i == j) ? (double)(mi ? mi : mj) : 0.0;
-                } else if (i < oq && j < oq) {  // yc x yc
-                    if (k == 0) val = (i == j) ? -1.0 : 0.0;
-                    else {
-                        val = (i == j) ? -dc : 0.0;
-                        if (k > 1) val -= Gp[(oq + i) * n + j] + h * Gp[(oqd + i) * n + j];
-                    }
-                } else if (i < oq || j < oq) {  // yc x primal
-                    int a = i < oq ? i : j, pv = i < oq ? j : i;
-                    val = (k > 0 && pv == oq + a) ? -1.0 : 0.0;
-                } else if (k < N) {
-                    bool pi = i < oyl, pj = j < oyl;
-                    if (pi && pj) {
-                        int u = i - oq, v = j - oq;
-                        double a = Wk[u * NV + v];
-                        for (int jj = 0; jj < n; jj++) a += Jtk[jj * NV + u] * Dd_s[jj] * Jtk[jj * NV + v];
-                        if (u == v) {
-                            a += dw + (u >= 2 * n ? dFr : 0.0);
-                            if (u < n) a += Sxq[k * n + u];
-                            else if (u < 2 * n) a += Sxd[k * n + u - n];
-                        }
-                        val = a;
-                    } else if (!pi && !pj) {
-                        val = (i == j) ? -dc : 0.0;
-                    } else {
-                        int l = pi ? j - oyl : i - oyl, pv = pi ? i - oq : j - oq;
-                        val = (pv < n) ? Jlk[l * n + pv] : 0.0;
-                    }
-                } else {  // terminal block: q_N diagonal
-                    val = (i == j) ? Sxq[N * n + (i - oq)] + dw : 0.0;
-                }
-                Dm[i * LD + j] = val;
-            }
-            // right-hand side (with the Schur contribution of the previous block)
-            for (int i = lane; i < m; i += 64) {
-                double r = 0.0;
-                if (masked(i)) {
-                    r = 0.0;
-                } else if (i < oq) {
-                    if (k > 0) {
-                        r = -(q[(k - 1) * n + i] + h * qd[(k - 1) * n + i] - q[k * n + i]);
-                        if (k > 1) r -= wp[oq + i] + h * wp[oqd + i];
-                    }
-                } else if (k < N) {
-                    if (i < oyl) {
-                        int u = i - oq;
-                        double g = gf[k * NV + u];
-                        for (int jj = 0; jj < n; jj++) g += Jtk[jj * NV + u] * (yd[k * n + jj] + Dd_s[jj] * rdd_s[jj]);
-                        if (u < n) {
-                            g += gphq[k * n + u] + yc[k * n + u] - (k > 0 ? yc[(k - 1) * n + u] : 0.0);
-                            for (int l = 0; l < nl; l++) g += Jlk[l * n + u] * yl[k * nl + l];
-                        } else if (u < 2 * n) {
-                            g += gphd[k * n + u - n] + h * yc[k * n + u - n];
-                        }
-                        r = -g;
-                    } else {
-                        r = -line[k * nl + (i - oyl)];
-                    }
+            // ---- stage block [[Quu, Du^T], [Du, -dc]] and right-hand sides -[Qux | qu ; G | e]
+            for (int e = lane; e < NK * NK; e += 64) {
+                int a = e / NK, c = e % NK;
+                double val;
+                if (a < NU && c < NU) {
+                    val = Hs[(n + a) * NV + n + c];
+                    if (a < n && c < n) val += h * h * Ps[a * n + c];
+                } else if (a >= NU && c >= NU) {
+                    val = (a == c) ? (con ? -dc : -1.0) : 0.0;
                 } else {
-                    int j = i - oq;
-                    r = -(gphq[N * n + j] - yc[(N - 1) * n + j]);
+                    int l = (a >= NU) ? a - NU : c - NU, v = (a >= NU) ? c : a;
+                    val = (con && v < n) ? h * Gl[l * n + v] : 0.0;
                 }
-                RH[i * NR + 0] = r;
-                for (int c = 0; c < n; c++)
-                    RH[i * NR + 1 + c] = (k > 0 && k < N) ? ((i == oq + c) ? 1.0 : (i == oqd + c ? h : 0.0)) : 0.0;
+                Ks[a * LDK + c] = val;
+            }
+            for (int e = lane; e < NK * NRK; e += 64) {
+                int a = e / NRK, c = e % NRK;
+                double val;
+                if (a < NU) {
+                    if (c < n) val = -(Hs[(n + a) * NV + c] + (a < n ? h * Ps[a * n + c] : 0.0));
+                    else val = -(gs[n + a] + (a < n ? h * ss[a] : 0.0));
+                } else {
+                    int l = a - NU;
+                    val = con ? -(c < n ? Gl[l * n + c] : el[l]) : 0.0;
+                }
+                Rk[e] = val;
             }
             __syncthreads();
-            BKInertia in = bk_factor_wave<LD>(Dm, m, perm, piv, c0, c1);
-            npos += in.pos; nneg += in.neg; nzero += in.zero;
-            if (in.zero) break;
-            const int nr = (k > 0 && k < N) ? NR : 1;
-            bk_solve_wave<LD, NR>(Dm, m, perm, piv, RH, nr, Yb);
-            for (int i = lane; i < m; i += 64) {
-                wv[(size_t)k * MB + i] = RH[i * NR];
-                if (k < N)
-                    for (int c = 0; c < n; c++) G[((size_t)k * MB + i) * n + c] = (k > 0) ? RH[i * NR + 1 + c] : 0.0;
+            BKInertia in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+            if (in.zero) { ok = false; zero = true; break; }
+            if (in.pos != NU || in.neg != NL) { ok = false; break; }
+            bk_solve_wave<LDK, NRK>(Ks, NK, perm, piv, Rk, NRK, Yk);
+            // ---- P_k = Qxx + Qxu Ku + G^T Kl ; p_k = qx + Qxu ku + G^T kl
+            for (int e = lane; e < n * n; e += 64) {
+                int i = e / n, j = e % n;
+                double a = Hs[i * NV + j] + Ps[i * n + j];
+                for (int c = 0; c < NU; c++) a += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[c * NRK + j];
+                if (con)
+                    for (int l = 0; l < nl; l++) a += Gl[l * n + i] * Rk[(NU + l) * NRK + j];
+                Pn[e] = a;
             }
-            __threadfence_block();
+            double pnew = 0.0;
+            if (lane < n) {
+                int i = lane;
+                pnew = gs[i] + ss[i];
+                for (int c = 0; c < NU; c++) pnew += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[c * NRK + n];
+                if (con)
+                    for (int l = 0; l < nl; l++) pnew += Gl[l * n + i] * Rk[(NU + l) * NRK + n];
+            }
+            for (int e = lane; e < NK * n; e += 64) Gk[e] = Rk[(e / n) * NRK + e % n];  // Ku (NU x n), Kl (NL x n)
+            for (int a = lane; a < NK; a += 64) wk[a] = Rk[a * NRK + n];              // ku, kl
+            __syncthreads();
+            for (int e = lane; e < n * n; e += 64) {
+                int i = e / n, j = e % n;
+                Ps[e] = 0.5 * (Pn[e] + Pn[j * n + i]);
+            }
+            if (lane < n) ps[lane] = pnew;
             __syncthreads();
         }
-        const int want_pos = N * NV + n, want_neg = N * (n + nl) + n;
-        if (nzero == 0 && npos == want_pos && nneg == want_neg) { factor_ok = true; break; }
-        if (nzero > 0 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
+        if (ok) { factor_ok = true; break; }
+        if (zero && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
         st.n_ic++;
-        if (tier == 1) {
-            if (dFr == 0.0) dFr = (dF_last0 == 0.0) ? 1e-4 : fmax(1e-20, dF_last0 / 3.0);
-            else dFr = (dF_last0 == 0.0) ? 100.0 * dFr : 8.0 * dFr;
-            if (dFr > 1e6) tier = 2;
-            else continue;
+        step_no++;
+        if (tier == 0) {
+            tier = (nf > 0 && C.wF < 0) ? 1 : 2;
+            reg = 1e-4;
+        } else if (step_no == 1 && reg_tier0 == tier && reg < reg_last0) {
+            reg = reg_last0;
+        } else {
+            reg *= 8.0;
+            if (tier == 1 && reg > 1e6) { tier = 2; reg = 1e-4; }
         }
-        if (dw == 0.0) dw = (dw_last0 == 0.0) ? 1e-4 : fmax(1e-20, dw_last0 / 3.0);
-        else dw = (dw_last0 == 0.0) ? 100.0 * dw : 8.0 * dw;
-        if (dw > 1e40) break;
+        if (reg > 1e40) break;
+        dFr = (tier == 1) ? reg : 0.0;
+        dw = (tier == 2) ? reg : 0.0;
     }
+    STAMP(2);
+    STAMP_COUNT(8, ntries);
     if (!factor_ok) { finish(ST_INERTIA); return; }
-    if (dw > 0) st.dw_last = dw;
-    st.dF_last = (tier == 1) ? dFr : 0.0;
+    st.reg_tier = tier;
+    st.reg_last = reg;
 
-    // ---------------- back substitution: y_N = w_N, y_k = w_k - G_k y_{k+1}[yc]
-    for (int i = lane; i < 2 * n; i += 64) ynext[i] = wv[(size_t)N * MB + i];
+    // ---------------- forward sweep: du_k = Ku dx_k + ku, dyl_{k+1} = Kl dx_k + kl,
+    //                  dyc_k = P_{k+1} dx_{k+1} + p_{k+1}
+    for (int j = lane; j < n; j += 64) {
+        dq[j] = 0.0; dqd[j] = 0.0;
+        xs[j] = q[j] + h * qd[j] - q[n + j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
+    }
+    for (int a = lane; a < nf; a += 64) dF[a] = wv[NJ + a];
+    for (int l = lane; l < nl; l += 64) { dyl[l] = 0.0; dyl[nl + l] = 0.0; }
     __syncthreads();
-    for (int j = lane; j < n; j += 64) { dq[N * n + j] = ynext[oq + j]; dyc[(N - 1) * n + j] = ynext[oyc + j]; }
-    for (int k = N - 1; k >= 0; k--) {
-        const double *wk = wv + (size_t)k * MB, *Gk = G + (size_t)k * MB * n;
-        for (int i = lane; i < MB; i += 64) {
-            double a = wk[i];
-            for (int c = 0; c < n; c++) a -= Gk[i * n + c] * ynext[oyc + c];
-            ybuf[i] = a;
+    for (int j = lane; j < n; j += 64) {  // dyc_0 = P_1 dx_1 + p_1 (slot 0)
+        double a = wv[NU + NL + j];
+        for (int i = 0; i < n; i++) a += G[(NU + NL) * n + j * n + i] * xs[i];
+        dyc[j] = a;
+    }
+    for (int k = 1; k < N; k++) {
+        const double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
+        for (int a = lane; a < NK; a += 64) {
+            double v = wk[a];
+            for (int i = 0; i < n; i++) v += Gk[a * n + i] * xs[i];
+            us[a] = v;
         }
+        for (int j = lane; j < n; j += 64) dq[k * n + j] = xs[j];
         __syncthreads();
-        for (int i = lane; i < MB; i += 64) {
-            double y = ybuf[i];
-            if (i < oq) { if (k > 0) dyc[(k - 1) * n + i] = y; }
-            else if (i < oqd) dq[k * n + i - oq] = y;
-            else if (i < oF) dqd[k * n + i - oqd] = y;
-            else if (i < oyl) dF[k * NFA + i - oF] = y;
-            else dyl[k * nl + i - oyl] = LINE_ON(k) ? y : 0.0;
-            ynext[i] = y;
+        for (int j = lane; j < n; j += 64) {
+            dqd[k * n + j] = us[j];
+            cs[j] = xs[j] + h * us[j] + (q[k * n + j] + h * qd[k * n + j] - q[(k + 1) * n + j]);
+        }
+        for (int a = lane; a < nf; a += 64) dF[k * NFA + a] = us[NJ + a];
+        if (k + 1 < N)
+            for (int l = lane; l < nl; l += 64) dyl[(k + 1) * nl + l] = ((nl > 0) && LINE_ON(k + 1)) ? us[NU + l] : 0.0;
+        __syncthreads();
+        for (int j = lane; j < n; j += 64) {
+            double a = wk[NU + NL + j];
+            for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * cs[i];
+            dyc[k * n + j] = a;
+            xs[j] = cs[j];
         }
         __syncthreads();
     }
-    for (int j = lane; j < n; j += 64) { dq[j] = 0.0; dqd[j] = 0.0; }
+    for (int j = lane; j < n; j += 64) dq[N * n + j] = xs[j];
     __threadfence_block();
     __syncthreads();
 
@@ -607,6 +698,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     __threadfence_block();
     __syncthreads();
 
+    STAMP(3);
     // ---------------- fraction to boundary
     double ap = 1.0, az = 1.0;
     auto ftbL = [&](double x, double dx, double lo, double &a) { if (dx < 0) a = fmin(a, -tau_fb * (x - lo) / dx); };
@@ -674,9 +766,37 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         theta = th;
         ok_out = (bad == 0);
     };
+    // merit at the current point from the node values the eval kernel stored
     double phi0, th0;
-    bool ok0;
-    merit(0.0, phi0, th0, ok0);
+    {
+        double f = 0, bar = 0, th = 0;
+        for (int k = lane; k < N; k += 64) {
+            f += cost[k];
+            for (int j = 0; j < n; j++) {
+                th += fabs(q[k * n + j] + h * qd[k * n + j] - q[(k + 1) * n + j]);
+                if (TACT(k, j)) th += fabs(tau[k * n + j] - s[k * n + j]);
+            }
+            if (LINE_ON(k))
+                for (int l = 0; l < nl; l++) th += fabs(line[k * nl + l]);
+        }
+        for (int e = n + lane; e < (N + 1) * n; e += 64) {
+            int j = e % n;
+            if (hasb(QLO[j])) bar -= log(q[e] - QLO[j]);
+            if (hasb(QHI[j])) bar -= log(QHI[j] - q[e]);
+        }
+        for (int e = lane; e < N * n; e += 64) {
+            int k = e / n, j = e % n;
+            if (k > 0) {
+                if (hasb(DLO[j])) bar -= log(qd[e] - DLO[j]);
+                if (hasb(DHI[j])) bar -= log(DHI[j] - qd[e]);
+            }
+            if (hasb(tlo[e])) bar -= log(s[e] - tlo[e]);
+            if (hasb(thi[e])) bar -= log(thi[e] - s[e]);
+        }
+        f = wave_sum(f); bar = wave_sum(bar); th = wave_sum(th);
+        phi0 = f + mu * bar;
+        th0 = th;
+    }
     double gdot = 0, pHp = 0;
     for (int k = lane; k < N; k += 64) {
         const double *Wk = W + (size_t)k * NV * NV;
@@ -702,8 +822,10 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         double nreq = (gdot + 0.5 * fmax(pHp, 0.0)) / ((1.0 - rho) * th0);
         if (nu < nreq) nu = nreq + 1.0;
     }
+    STAMP(4);
     const double Dphi = gdot - nu * th0;
     const double m0 = phi0 + nu * th0;
+    int nls = 0;
     double alpha = ap;
     bool accepted = false;
     for (int ls = 0; ls < 40; ls++) {
@@ -711,12 +833,15 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         bool okk;
         merit(alpha, ph, th, okk);
         double mt = ph + nu * th;
+        nls++;
         if (okk && isfinite(mt) && mt - m0 <= eta * alpha * fmin(Dphi, 0.0) + 10.0 * 2.220446049250313e-16 * fabs(m0)) {
             accepted = true;
             break;
         }
         alpha *= 0.5;
     }
+    STAMP(5);
+    STAMP_COUNT(9, nls);
     if (!accepted) {
         st.n_ls_fail++;
         st.consec_fail++;
@@ -754,6 +879,8 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         if (hasb(tlo[e])) zupd(vL[e], dvL[e], s[e] - tlo[e]);
         if (hasb(thi[e])) zupd(vU[e], dvU[e], thi[e] - s[e]);
     }
+    STAMP(6);
+    STAMP_COUNT(10, 1);
     if (lane == 0) {
         st.iter++;
         st.mu = mu;
@@ -802,16 +929,20 @@ struct IpmLaunch {
                      hipStream_t s) {
         hipLaunchKernelGGL((k_ipm_init<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
     }
-    static void iter(const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A, int batch,
-                     hipStream_t s) {
+    // phase 0: node values + Jacobians, 1: Lagrangian Hessians, 2: per-problem IPM step
+    static void iter(int phase, const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A,
+                     int batch, hipStream_t s) {
         constexpr int NV = 2 * NJ + NF;
         constexpr int NP = NV * (NV + 1) / 2;
         long tj = (long)batch * C.N * NV, th = (long)batch * C.N * NP;
-        hipLaunchKernelGGL((k_eval_jac<NJ, NF>), dim3((unsigned)((tj + 255) / 256)), dim3(256), 0, s, M, F, C, A,
-                           batch);
-        hipLaunchKernelGGL((k_eval_hess<NJ, NF>), dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, M, F, C, A,
-                           batch);
-        hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+        if (phase == 0)
+            hipLaunchKernelGGL((k_eval_jac<NJ, NF>), dim3((unsigned)((tj + 255) / 256)), dim3(256), 0, s, M, F, C,
+                               A, batch);
+        else if (phase == 1)
+            hipLaunchKernelGGL((k_eval_hess<NJ, NF>), dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, M, F,
+                               C, A, batch);
+        else
+            hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
     }
     static void output(const OcpConst &C, const IpmArrays &A, int batch, double *w, int *status, int *iters,
                        double *kkt, double *obj, hipStream_t s) {
@@ -831,7 +962,7 @@ bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevF
 #define MF_CASE(NJ, NF, NL)                                                       \
     if (n == NJ && nf == NF && nl == NL) {                                        \
         if (what == 0) IpmLaunch<NJ, NF, NL>::init(M, F, C, A, batch, s);          \
-        else if (what == 1) IpmLaunch<NJ, NF, NL>::iter(M, F, C, A, batch, s);     \
+        else if (what >= 10 && what <= 12) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
         else IpmLaunch<NJ, NF, NL>::output(C, A, batch, w, status, iters, kkt, obj, s); \
         return true;                                                              \
     }
@@ -843,3 +974,10 @@ bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevF
 }
 
 }  // namespace mf
+
+#ifdef MF_PHASE_STAMPS
+extern "C" int mf_debug_phase_stamps(unsigned long long *out, int nprob) {
+    if (nprob > 4096) nprob = 4096;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mf::mf_stamp_buf), sizeof(unsigned long long) * 16 * nprob) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -101,6 +101,17 @@ class OCP:
         _lib.check(_lib.lib().mf_solve_batch_dev(self._h, batch, q0_ptr, lref_ptr, C.byref(o), out["w"],
                                                  out["status"], out["iters"], out["kkt"], out["obj"], stream))
 
+    KERNELS = ("k_eval_jac", "k_eval_hess", "k_ipm_iter")
+
+    def timing(self, enable: bool = True) -> None:
+        _lib.check(_lib.lib().mf_problem_timing(self._h, int(enable)))
+
+    def kernel_stats(self) -> dict:
+        ms = np.zeros(3)
+        n = (C.c_long * 3)()
+        _lib.check(_lib.lib().mf_problem_kernel_stats(self._h, _lib.dptr(ms), n))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
+
     def node_eval(self, x, u, line_ref=None):
         """(x, u) -> (xnext, g, cost, jac) for a batch of shooting nodes (mf_node_eval)."""
         n, nf, nl = self.n, self.nf, self.nl

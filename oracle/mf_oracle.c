@@ -699,7 +699,8 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
 
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
     const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
-    double mu = O->mu_init, nu = 0.0, dw_last = 0.0, dF_last = 0.0;
+    double mu = O->mu_init, nu = 0.0, reg_last = 0.0;
+    int reg_tier = 0;
     int status = 1, it = 0, n_ls_fail = 0, n_ic = 0, consecutive_fail = 0;
     double E0 = INFINITY, cviol = INFINITY;
 
@@ -846,8 +847,16 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
          * (block k), i.e. K_{k+1,k} = C = [0 I hI 0 0] restricted to the yc rows.
          * Forward block elimination D_{k+1}[yc,yc] -= C D_k^-1 C^T, G_k = D_k^-1 C^T. */
         const int oyc = 0, oq = n, oqd = 2 * n, oF = 3 * n, oyl = 3 * n + nf;
+        /* Inertia correction: tier 1 regularises only the force block
+         * (the concave -F^2 directions), tier 2 the whole primal block.  The previous
+         * iteration's tier and value are remembered; attempts: last/3, last, then x8
+         * (0 once the value has decayed below 1e-8).  Tier 1 escalates into tier 2 above 1e6. */
         double dw = 0.0, dc = 0.0, dF = 0.0, dprox = O->prox * mu;
-        int tries = 0, factor_ok = 0, tier = (nf > 0 && P->wF < 0) ? 1 : 2;
+        int tries = 0, factor_ok = 0;
+        int tier = reg_tier, step_no = 0;
+        double reg = (reg_tier == 0) ? 0.0 : reg_last / 3.0;
+        if (reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
+        if (tier == 1) dF = reg; else if (tier == 2) dw = reg;
         for (tries = 0; tries < 60; tries++) {
             int npos_t = 0, nneg_t = 0, nzero_t = 0;
             for (int k = 0; k <= N; k++) {
@@ -955,20 +964,23 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
             if (nzero_t == 0 && npos_t == want_pos && nneg_t == want_neg) { factor_ok = 1; break; }
             if (nzero_t > 0 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
             n_ic++;
-            if (tier == 1) {
-                /* structured correction: regularise the concave force block first */
-                if (dF == 0.0) dF = (dF_last == 0.0) ? 1e-4 : fmax(1e-20, dF_last / 3.0);
-                else dF = (dF_last == 0.0) ? 100.0 * dF : 8.0 * dF;
-                if (dF > 1e6) { tier = 2; }
-                else continue;
+            step_no++;
+            if (tier == 0) {
+                tier = (nf > 0 && P->wF < 0) ? 1 : 2;
+                reg = 1e-4;
+            } else if (step_no == 1 && reg_tier == tier && reg < reg_last) {
+                reg = reg_last;               /* last/3 failed: retry the value that worked */
+            } else {
+                reg *= 8.0;
+                if (tier == 1 && reg > 1e6) { tier = 2; reg = 1e-4; }
             }
-            if (dw == 0.0) dw = (dw_last == 0.0) ? 1e-4 : fmax(1e-20, dw_last / 3.0);
-            else dw = (dw_last == 0.0) ? 100.0 * dw : 8.0 * dw;
-            if (dw > 1e40) break;
+            if (reg > 1e40) break;
+            dF = (tier == 1) ? reg : 0.0;
+            dw = (tier == 2) ? reg : 0.0;
         }
         if (!factor_ok) { status = 3; break; }
-        if (dw > 0) dw_last = dw;
-        dF_last = (tier == 1) ? dF : 0.0;
+        reg_tier = tier;
+        reg_last = reg;
         if (O->verbose > 1) fprintf(stderr, "   dF %.2e dw %.2e dc %.2e tries %d\n", dF, dw, dc, tries);
 
         /* ---- back substitution: y_N = w_N, y_k = w_k - G_k y_{k+1}[yc] ---- */

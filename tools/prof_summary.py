@@ -1,0 +1,23 @@
+"""Summarise a rocprofv3 --kernel-trace --stats database into profiles/ (markdown)."""
+import glob
+import sqlite3
+import sys
+
+
+def main(db_glob: str, out: str, title: str):
+    db = sorted(glob.glob(db_glob, recursive=True))[0]
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    with open(out, "w") as f:
+        f.write(f"# {title}\n\nSource: `{db}` (rocprofv3 --kernel-trace --stats), durations in microseconds.\n\n")
+        f.write("| kernel | calls | total us | avg us | % |\n|---|---|---|---|---|\n")
+        for name, calls, tot, avg, pct in rows:
+            short = name.split("(")[0].replace("void ", "")
+            if len(short) > 80:
+                short = short[:77] + "..."
+            f.write(f"| `{short}` | {calls} | {tot:.1f} | {avg:.3f} | {pct:.2f} |\n")
+    print(open(out).read())
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "rocprofv3 kernel summary")
