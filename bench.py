@@ -36,22 +36,22 @@ FP64_PEAK_TFS = 78.6          # MI355X FP64 vector peak (spec)
 def node_bytes(n: int, nf: int, nl: int) -> dict:
     """Algorithmic HBM bytes per shooting node of one running horizon per launch.
 
-    k_eval_jac : reads q, qd, F; writes tau, line, cost, dtau/dw, dline/dq, grad f
-    k_eval_hess: reads q, qd, F, tau, y_tau, y_line, dtau/dw; writes the stage Hessian W
-    k_ipm_iter : reads the node data once (W, dtau/dw, grad f, tau, line, dline/dq, cost), reads and
-                 writes the iterate once (q, qd, F, s, y_c, y_line, y_tau, 4 bound-multiplier sets,
-                 2 slack-multiplier sets), writes and reads back the Riccati slot once
-                 (Ku, Kl, P_{k+1}, ku, kl, p_{k+1})
+    k_eval_node: reads the node's q, qd, F, y_tau, y_line, torque slacks and their
+                 multipliers, the fatigue bounds and the q/qd bound multipliers; writes
+                 tau, line, cost, d tau/dw, d line/dq, grad f and the condensed stage
+                 Hessian H0 (nv x nv)
+    k_ipm_iter : reads the node data once (H0, d tau/dw, grad f, tau, line, dline/dq, cost),
+                 reads and writes the iterate once (q, qd, F, s, y_c, y_line, y_tau, 4
+                 bound-multiplier sets, 2 slack-multiplier sets), writes and reads back the
+                 Riccati slot once (Ku, Kl, P_{k+1}, ku, kl, p_{k+1})
     """
     nv, nu = 2 * n + nf, n + nf
-    x = 8 * (n + n + nf)
-    jac = 8 * (n + nl + 1 + n * nv + nl * n + nv)
-    hess = 8 * (n + n + nl + n * nv) + 8 * nv * nv
+    rd = (n + n + nf) + n + nl + 3 * n + 2 * n + 4 * n
+    wr = n + nl + 1 + n * nv + nl * n + nv + nv * nv
     node = nv * nv + n * nv + nv + n + nl + nl * n + 1
     state = (n + n + nf + n + n + nl + n) + 2 * n + 2 * n + 2 * n
     slot = nu * n + nl * n + n * n + nu + nl + n
-    ipm = 8 * (node + 2 * state + 2 * slot)
-    return {"k_eval_jac": x + jac, "k_eval_hess": x + hess, "k_ipm_iter": ipm}
+    return {"k_eval_node": 8 * (rd + wr), "k_ipm_iter": 8 * (node + 2 * state + 2 * slot)}
 
 
 def main() -> int:

@@ -126,11 +126,14 @@ int mf_solve_batch_dev(mf_problem *p, int batch, const double *q0, const double 
                        const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt, double *obj,
                        void *stream);
 
-/* Per-kernel device time of the solver's launches on the solve stream (HIP events):
- * index 0 = node values + Jacobians (k_eval_jac), 1 = Lagrangian Hessians
- * (k_eval_hess), 2 = per-problem IPM step (k_ipm_iter).  Enabling resets the totals. */
+/* Per-kernel device time of the solver's launches on the solve stream (HIP events),
+ * MF_NKERNELS slots named by mf_kernel_name(slot): 0 = node values, Jacobians and
+ * condensed stage Hessians (k_eval_node), 1 = per-problem IPM step (k_ipm_iter),
+ * 2 = reserved (0).  Enabling resets the totals. */
+#define MF_NKERNELS 3
 int mf_problem_timing(mf_problem *p, int enable);
-int mf_problem_kernel_stats(const mf_problem *p, double *ms_total3, long *launches3);
+int mf_problem_kernel_stats(const mf_problem *p, double *ms_total, long *launches);
+const char *mf_kernel_name(int slot);
 
 const char *mf_last_error(void);
 

@@ -46,43 +46,6 @@ static int ensure_device() {
     return MF_OK;
 }
 
-namespace mf {
-DevModel make_dev_model(const Model &M) {
-    DevModel D;
-    memset(&D, 0, sizeof D);
-    D.n = (int)M.joints.size();
-    D.serial = 1;
-    for (int k = 0; k < 3; k++) D.g[k] = M.gravity[k];
-    for (int i = 0; i < D.n; i++) {
-        const Joint &J = M.joints[i];
-        DevJoint &d = D.j[i];
-        memcpy(d.RX, J.R, sizeof d.RX);
-        memcpy(d.tX, J.t, sizeof d.tX);
-        memcpy(d.axis, J.axis, sizeof d.axis);
-        const double *a = J.axis;
-        double K[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
-        memcpy(d.K, K, sizeof K);
-        for (int r = 0; r < 3; r++)
-            for (int c = 0; c < 3; c++) d.K2[3 * r + c] = K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c] + K[3 * r + 2] * K[6 + c];
-        d.m = J.mass;
-        memcpy(d.c, J.com, sizeof d.c);
-        memcpy(d.Ic, J.Ic, sizeof d.Ic);
-        d.parent = J.parent;
-        if (J.parent != i - 1) D.serial = 0;
-    }
-    return D;
-}
-DevFrame make_dev_frame(const Model &M, int frame) {
-    DevFrame F;
-    memset(&F, 0, sizeof F);
-    const Frame &f = M.frames[frame];
-    F.parent = f.parent;
-    memcpy(F.R, f.R, sizeof F.R);
-    memcpy(F.t, f.t, sizeof F.t);
-    return F;
-}
-}  // namespace mf
-
 struct mf_model {
     Model host;
     DevModel dev;
@@ -357,8 +320,8 @@ struct mf_problem {
     // per-kernel timing (HIP events on the solve stream), enabled by mf_problem_timing
     int timing = 0;
     std::vector<hipEvent_t> ev;
-    double t_ms[3] = {0, 0, 0};
-    long t_launch[3] = {0, 0, 0};
+    double t_ms[MF_NKERNELS] = {0};
+    long t_launch[MF_NKERNELS] = {0};
     // solver workspace (grown on demand)
     int cap = 0;
     std::vector<double *> bufs;
@@ -505,28 +468,28 @@ static int solve_core(mf_problem *p, int batch, const double *d_q0, const double
         return fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
     HIPCHK(hipGetLastError());
     int active = batch;
-    const int chunk = 4;
-    if (p->timing && p->ev.size() < (size_t)(6 * chunk)) {
+    const int chunk = 4, NPH = 2;  // launches per iteration: k_eval_node, k_ipm_iter
+    if (p->timing && p->ev.size() < (size_t)(2 * NPH * chunk)) {
         for (auto e2 : p->ev) (void)hipEventDestroy(e2);
-        p->ev.assign(6 * chunk, nullptr);
+        p->ev.assign(2 * NPH * chunk, nullptr);
         for (auto &e2 : p->ev) HIPCHK(hipEventCreate(&e2));
     }
     for (int it = 0; it <= C.max_iter && active > 0; it += chunk) {
         for (int c = 0; c < chunk; c++)
-            for (int ph = 0; ph < 3; ph++) {
-                if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * 3 + ph) * 2], s));
+            for (int ph = 0; ph < NPH; ph++) {
+                if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * NPH + ph) * 2], s));
                 ipm_dispatch(n, C.nf, C.nl, 10 + ph, p->model->d_model, F, C, A, batch, s, nullptr, nullptr, nullptr,
                              nullptr, nullptr);
-                if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * 3 + ph) * 2 + 1], s));
+                if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * NPH + ph) * 2 + 1], s));
             }
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (p->timing)
             for (int c = 0; c < chunk; c++)
-                for (int ph = 0; ph < 3; ph++) {
+                for (int ph = 0; ph < NPH; ph++) {
                     float ms = 0;
-                    HIPCHK(hipEventElapsedTime(&ms, p->ev[(c * 3 + ph) * 2], p->ev[(c * 3 + ph) * 2 + 1]));
+                    HIPCHK(hipEventElapsedTime(&ms, p->ev[(c * NPH + ph) * 2], p->ev[(c * NPH + ph) * 2 + 1]));
                     p->t_ms[ph] += ms;
                     p->t_launch[ph]++;
                 }
@@ -672,12 +635,31 @@ extern "C" int mf_node_eval(const mf_problem *pc, const double *x, const double 
 extern "C" int mf_problem_timing(mf_problem *p, int enable) {
     if (!p) return fail(MF_ERR_ARG, "null problem");
     p->timing = enable ? 1 : 0;
-    for (int k = 0; k < 3; k++) { p->t_ms[k] = 0; p->t_launch[k] = 0; }
+    for (int k = 0; k < MF_NKERNELS; k++) { p->t_ms[k] = 0; p->t_launch[k] = 0; }
     return MF_OK;
+}
+
+extern "C" const char *mf_kernel_name(int slot) {
+    static const char *names[MF_NKERNELS] = {"k_eval_node", "k_ipm_iter", ""};
+    return (slot >= 0 && slot < MF_NKERNELS) ? names[slot] : "";
 }
 
 extern "C" int mf_problem_kernel_stats(const mf_problem *p, double *ms_total3, long *launches3) {
     if (!p || !ms_total3 || !launches3) return fail(MF_ERR_ARG, "null argument");
-    for (int k = 0; k < 3; k++) { ms_total3[k] = p->t_ms[k]; launches3[k] = p->t_launch[k]; }
+    for (int k = 0; k < MF_NKERNELS; k++) { ms_total3[k] = p->t_ms[k]; launches3[k] = p->t_launch[k]; }
     return MF_OK;
 }
+
+#ifdef MF_TRACE
+// Diagnostic build only: copy `count` doubles of one solver array (problem 0 first) to the host.
+// which: 0 q 1 qd 2 F 3 s 4 yc 5 yl 6 yd 7 zqL 8 zqU 9 zdL 10 zdU 11 vL 12 vU 13 tau 14 Jt
+//        15 Jl 16 W 17 gf 18 line 19 cost
+extern "C" int mf_debug_array(const mf_problem *p, int which, double *out, long count) {
+    const IpmArrays &A = p->A;
+    double *src[20] = {A.q, A.qd, A.F, A.s, A.yc, A.yl, A.yd, A.zqL, A.zqU, A.zdL, A.zdU, A.vL, A.vU,
+                       A.tau, A.Jt, A.Jl, A.W, A.gf, A.line, A.cost};
+    if (which < 0 || which >= 20 || !src[which]) return -1;
+    return hipMemcpy(out, src[which], sizeof(double) * count, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+

@@ -1,19 +1,19 @@
 // Batched interior-point solve of the fatigue-aware OCP on MI355X (gfx950).
 //
-// One IPM iteration = three launches:
-//   k_eval_jac  lanes (problem, node, direction u)   dual numbers: tau, line, cost
-//                                                     and column u of their Jacobian
-//   k_eval_hess lanes (problem, node, pair (u<=v))    hyper-dual numbers: entry (u,v)
-//                                                     of the stage Lagrangian Hessian
+// One IPM iteration = two launches:
+//   k_eval_node lanes (problem, node, direction v)   forward-over-reverse dual sweep
+//               (adj.hpp): tau, line, cost, column v of their Jacobian and of the exact
+//               Lagrangian Hessian; writes the condensed stage Hessian H0
 //   k_ipm_iter  one wavefront per problem             optimality error, barrier update,
-//               inertia-corrected block-tridiagonal LDL^T (Bunch-Kaufman stage blocks
-//               in LDS), step recovery, fraction-to-boundary, l1-merit line search,
+//               inertia-corrected Riccati recursion (Bunch-Kaufman stage blocks in LDS),
+//               step recovery, fraction-to-boundary, l1-merit line search (node_values),
 //               update.  Mirrors oracle/mf_oracle.c mfo_solve statement by statement.
 // Model constants (URDF joint placements, inertias) are staged in LDS per
 // workgroup; per-problem arrays are [problem][node][field] so a wave reading a
 // node's data, and lanes (node, field) writing it, both touch contiguous bytes.
 #include <hip/hip_runtime.h>
 
+#include "adj.hpp"
 #include "bk_wave.hpp"
 #include "dyn.hpp"
 #include "ipm.hpp"
@@ -23,6 +23,14 @@ namespace mf {
 #define LINE_ON(k) ((k) >= 2)
 
 __device__ __forceinline__ bool hasb(double b) { return isfinite(b); }
+
+// primal-dual barrier Hessian of a scalar x in [lo, hi] (missing bound: +-inf, multiplier 0)
+__device__ __forceinline__ double sigma_pair(double zL, double zU, double x, double lo, double hi) {
+    double s = 0.0;
+    if (hasb(lo)) s += zL / (x - lo);
+    if (hasb(hi)) s += zU / (hi - x);
+    return s;
+}
 
 // Diagnostic build only (-DMF_PHASE_STAMPS): per-phase cycle counts of k_ipm_iter,
 // accumulated by lane 0 into a debug buffer (never read by the solver).
@@ -42,6 +50,35 @@ __device__ unsigned long long mf_stamp_buf[16 * 4096];
 #define STAMP_COUNT(slot, v) do {} while (0)
 #endif
 
+// IPOPT bound_push / bound_frac = 1e-2: move an initial value strictly inside its bounds
+__device__ __forceinline__ double bound_push(double x, double lo, double hi) {
+    const double k1 = 1e-2, k2 = 1e-2;
+    bool hl = hasb(lo), hh = hasb(hi);
+    if (hl && hh) {
+        double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
+        double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
+        x = fmax(x, lo + pl);
+        x = fmin(x, hi - pu);
+    } else if (hl) {
+        x = fmax(x, lo + k1 * fmax(1.0, fabs(lo)));
+    } else if (hh) {
+        x = fmin(x, hi - k1 * fmax(1.0, fabs(hi)));
+    }
+    return x;
+}
+
+// Diagnostic build only (-DMF_TRACE): per-iteration record of the first 16 problems
+// (16 doubles per iteration, read by mf_debug_trace; tools/trace_probe.py).
+#ifdef MF_TRACE
+__device__ double mf_trace_buf[16 * 512 * 16];
+#define TRACE(slot, val)                                                                     \
+    do {                                                                                     \
+        if (lane == 0 && b < 16 && st.iter < 512) mf_trace_buf[(b * 512 + st.iter) * 16 + (slot)] = (val); \
+    } while (0)
+#else
+#define TRACE(slot, val) do {} while (0)
+#endif
+
 // cooperative copy of a POD struct into LDS
 template <class T> __device__ __forceinline__ void stage_lds(T *dst, const T *src) {
     const int words = (int)(sizeof(T) / sizeof(double));
@@ -50,134 +87,187 @@ template <class T> __device__ __forceinline__ void stage_lds(T *dst, const T *sr
     for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
 }
 
-// ============================================================== eval: Jacobian lanes
-template <int NJ, int NF>
-__global__ __launch_bounds__(256) void k_eval_jac(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
-                                                  OcpConst C, IpmArrays A, int batch) {
-    __shared__ DevModel M;
-    __shared__ DevFrame F;
-    stage_lds(&M, Mg);
-    stage_lds(&F, Fg);
-    __syncthreads();
+// ============================================================== eval: node derivatives
+// Lanes (problem, node, direction v), NV = 2 n + n_f lanes per node, NPB nodes per
+// block.  Each lane runs node_fwd_rev<Dual> (adj.hpp) with tangent e_v and gets tau,
+// column v of d tau / dw, the line Jacobian column and column v of the exact Hessian
+// of phi = c.tau + yl.line, c = y_tau + 2 wtau tau.  The block exchanges the Jacobian
+// columns through LDS to add the Gauss-Newton / barrier term and writes the condensed
+// stage Hessian  H0_k = grad^2 L_k + J^T diag(2 wtau + Sigma_s) J + diag(Sigma_x)
+// (what the Riccati recursion needs at delta_w = delta_c = 0).
+template <int NJ, int NF> struct NodeIn {
+    const double *xq, *xqd;
+    int v;
+    __device__ __forceinline__ Dual q(int i) const { return Dual(xq[i], v == i ? 1.0 : 0.0); }
+    __device__ __forceinline__ Dual qd(int i) const { return Dual(xqd[i], v == NJ + i ? 1.0 : 0.0); }
+};
+template <int NJ, int NF, int NPB, int NV> struct NodeOut {
+    double (*Js)[NJ][NV];  // LDS: Jacobian columns of the block's nodes
+    double (*Hs)[NV][NV];  // LDS: Hessian columns of phi
+    double (*Ts)[NJ];      // LDS: tau values
+    int g, v;
+    const double *fdir;
+    double pfv[3], pfd[3];
+    __device__ __forceinline__ void frame(const Dual *p) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) { pfv[k] = p[k].v; pfd[k] = p[k].d; }
+    }
+    __device__ __forceinline__ void force(const Dual *gF) {
+#pragma unroll
+        for (int a = 0; a < NF; a++)
+            Hs[g][2 * NJ + a][v] = fdir[3 * a] * gF[0].d + fdir[3 * a + 1] * gF[1].d + fdir[3 * a + 2] * gF[2].d;
+    }
+    __device__ __forceinline__ void joint(int i, const Dual &t, const Dual &gq, const Dual &gqd) {
+        Js[g][i][v] = t.d;
+        if (v == 0) Ts[g][i] = t.v;
+        Hs[g][i][v] = gq.d;
+        Hs[g][NJ + i][v] = gqd.d;
+    }
+};
+
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                                   OcpConst C, IpmArrays A, int batch) {
     constexpr int NV = 2 * NJ + NF;
     constexpr int NFA = NF > 0 ? NF : 1;
-    long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    long total = (long)batch * C.N * NV;
-    if (t >= total) return;
-    const int u = (int)(t % NV);
-    const long r = t / NV;
-    const int k = (int)(r % C.N);
-    const int b = (int)(r / C.N);
-    if (A.st[b].status != ST_RUNNING) return;
+    constexpr int NPB = 256 / NV;
+    __shared__ DevModel M;
+    __shared__ DevFrame F;
+    __shared__ double Js[NPB][NJ][NV], Hs[NPB][NV][NV], Ts[NPB][NJ], Cs[NPB][NJ];
+    stage_lds(&M, Mg);
+    stage_lds(&F, Fg);
+    const int tid = threadIdx.x, g = tid / NV, v = tid % NV;
+    const int N = C.N;
+    const long node = (long)blockIdx.x * NPB + g;
+    bool run = (g < NPB) && node < (long)batch * N;
+    int b = 0, k = 0;
+    if (run) {
+        b = (int)(node / N);
+        k = (int)(node % N);
+        run = A.st[b].status == ST_RUNNING;
+    }
     const IpmSizes S = ipm_sizes(C);
     const double *q = A.q + b * S.q + (size_t)k * NJ;
     const double *qd = A.qd + b * S.u + (size_t)k * NJ;
     const double *Fv = A.F + b * S.f + (size_t)k * NFA;
-    Dual xq[NJ], xqd[NJ], xF[NFA], tau[NJ], pf[3];
+    NodeOut<NJ, NF, NPB, NV> out;
+    out.Js = Js;
+    out.Hs = Hs;
+    out.Ts = Ts;
+    out.g = g;
+    out.v = v;
+    out.fdir = C.fdir;
+    // torque weights c = y_tau + 2 wtau tau (tau at the iterate first when wtau != 0)
+    if (run && v == 0) {
+        const double *yd = A.yd + b * S.u + (size_t)k * NJ;
+        if (C.wtau != 0.0) {
+            struct WOut {
+                double *c;
+                const double *yd;
+                double w2;
+                __device__ void frame(const double *) {}
+                __device__ void force(const double *) {}
+                __device__ void joint(int j, double t, double, double) { c[j] = yd[j] + w2 * t; }
+            } wo{Cs[g], yd, 2.0 * C.wtau};
+            double Fw[3];
 #pragma unroll
-    for (int i = 0; i < NJ; i++) {
-        xq[i] = Dual(q[i], u == i ? 1.0 : 0.0);
-        xqd[i] = Dual(qd[i], u == NJ + i ? 1.0 : 0.0);
+            for (int r = 0; r < 3; r++) {
+                double acc = 0.0;
+#pragma unroll
+                for (int a = 0; a < NF; a++) acc += Fv[a] * C.fdir[3 * a + r];
+                Fw[r] = acc;
+            }
+            ArrIn<NJ> in0{q, qd};
+            node_values<NJ>(M, F, (NF > 0 || NL > 0) ? F.parent : -1, in0, Fw, wo);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NJ; j++) Cs[g][j] = yd[j];
+        }
     }
+    __syncthreads();
+    if (run) {
+        double yl3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-    for (int a = 0; a < NFA; a++) xF[a] = Dual(NF > 0 ? Fv[a] : 0.0, u == 2 * NJ + a ? 1.0 : 0.0);
-    node_tau<Dual, NJ>(M, F, NF, C.fdir, xq, xqd, xF, tau, pf);
+        for (int l = 0; l < NL; l++) yl3[l] = A.yl[b * S.l + (size_t)k * NL + l];
+        Dual Fw[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            Dual acc(0.0);
+#pragma unroll
+            for (int a = 0; a < NF; a++) acc += Dual(Fv[a], v == 2 * NJ + a ? 1.0 : 0.0) * C.fdir[3 * a + r];
+            Fw[r] = acc;
+        }
+        const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
+        NodeIn<NJ, NF> in{q, qd, v};
+        node_fwd_rev<Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
+    }
+    __syncthreads();
+    if (!run) return;
+    // barrier Hessian of the node: Sigma_s (torque slacks), Sigma_x (q_k, qd_k bounds, k >= 1)
+    const double *tlo = A.tau_lo + (size_t)k * NJ, *thi = A.tau_hi + (size_t)k * NJ;
+    const double *sk = A.s + b * S.u + (size_t)k * NJ;
+    const double *vL = A.vL + b * S.u + (size_t)k * NJ, *vU = A.vU + b * S.u + (size_t)k * NJ;
+    double wj[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; j++) wj[j] = 2.0 * C.wtau + sigma_pair(vL[j], vU[j], sk[j], tlo[j], thi[j]);
+    double diag = 0.0;
+    if (k > 0) {
+        if (v < NJ) {
+            const size_t e = b * S.q + (size_t)k * NJ + v;
+            diag = sigma_pair(A.zqL[e], A.zqU[e], q[v], C.q_lo[v], C.q_hi[v]);
+        } else if (v < 2 * NJ) {
+            const size_t e = b * S.u + (size_t)k * NJ + v - NJ;
+            diag = sigma_pair(A.zdL[e], A.zdU[e], qd[v - NJ], C.qd_lo[v - NJ], C.qd_hi[v - NJ]);
+        }
+    }
+    if (v >= NJ && v < 2 * NJ) diag += 2.0 * C.wqd;
+    if (v >= 2 * NJ) diag += 2.0 * C.wF;
+    double *W = A.W + b * S.w + (size_t)k * NV * NV;
+#pragma unroll
+    for (int u = 0; u < NV; u++) {
+        if (u < v) continue;
+        double gn = 0.0;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) gn += wj[j] * Js[g][j][u] * Js[g][j][v];
+        double hh = Hs[g][u][v] + gn;
+        if (u == v) hh += diag;
+        W[u * NV + v] = hh;
+        W[v * NV + u] = hh;
+    }
     double *Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
+    double gfv = 0.0;
 #pragma unroll
-    for (int j = 0; j < NJ; j++) Jt[j * NV + u] = tau[j].d;
-    if (C.nl > 0 && u < NJ) {
-        double *Jl = A.Jl + b * S.jl + (size_t)k * C.nl * NJ;
-        for (int l = 0; l < C.nl; l++) Jl[l * NJ + u] = pf[l].d;
+    for (int j = 0; j < NJ; j++) {
+        const double jv = Js[g][j][v];
+        Jt[j * NV + v] = jv;
+        gfv += 2.0 * C.wtau * Ts[g][j] * jv;
     }
-    double g = 0.0;
+    if (v >= NJ && v < 2 * NJ) gfv += 2.0 * C.wqd * qd[v - NJ];
+    if (NF > 0 && v >= 2 * NJ) gfv += 2.0 * C.wF * Fv[v - 2 * NJ];
+    A.gf[b * S.gf + (size_t)k * NV + v] = gfv;
+    if (NL > 0 && v < NJ) {
+        double *Jl = A.Jl + b * S.jl + (size_t)k * NL * NJ;
 #pragma unroll
-    for (int j = 0; j < NJ; j++) g += 2.0 * C.wtau * tau[j].v * tau[j].d;
-    if (u >= NJ && u < 2 * NJ) g += 2.0 * C.wqd * qd[u - NJ];
-    if (NF > 0 && u >= 2 * NJ) g += 2.0 * C.wF * Fv[u - 2 * NJ];
-    A.gf[b * S.gf + (size_t)k * NV + u] = g;
-    if (u == 0) {
-        double *tv = A.tau + b * S.u + (size_t)k * NJ;
+        for (int l = 0; l < NL; l++) Jl[l * NJ + v] = out.pfd[l];
+    }
+    if (v == 0) {
+        double *tvo = A.tau + b * S.u + (size_t)k * NJ;
         double c = 0.0;
+#pragma unroll
         for (int a = 0; a < NF; a++) c += C.wF * Fv[a] * Fv[a];
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
-            tv[j] = tau[j].v;
-            c += C.wqd * qd[j] * qd[j] + C.wtau * tau[j].v * tau[j].v;
+            const double tj = Ts[g][j];
+            tvo[j] = tj;
+            c += C.wqd * qd[j] * qd[j] + C.wtau * tj * tj;
         }
         A.cost[b * S.cost + k] = c;
-        if (C.nl > 0) {
-            double *lv = A.line + b * S.l + (size_t)k * C.nl;
-            for (int l = 0; l < C.nl; l++) lv[l] = pf[l].v - A.lref[b * 2 + l];
+        if (NL > 0) {
+            double *lv = A.line + b * S.l + (size_t)k * NL;
+#pragma unroll
+            for (int l = 0; l < NL; l++) lv[l] = out.pfv[l] - A.lref[b * 2 + l];
         }
     }
-}
-
-// ============================================================== eval: Hessian lanes
-template <int NJ, int NF>
-__global__ __launch_bounds__(256) void k_eval_hess(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
-                                                   OcpConst C, IpmArrays A, int batch) {
-    __shared__ DevModel M;
-    __shared__ DevFrame F;
-    stage_lds(&M, Mg);
-    stage_lds(&F, Fg);
-    __syncthreads();
-    constexpr int NV = 2 * NJ + NF;
-    constexpr int NFA = NF > 0 ? NF : 1;
-    constexpr int NP = NV * (NV + 1) / 2;
-    long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    long total = (long)batch * C.N * NP;
-    if (t >= total) return;
-    int p = (int)(t % NP);
-    const long r = t / NP;
-    const int k = (int)(r % C.N);
-    const int b = (int)(r / C.N);
-    if (A.st[b].status != ST_RUNNING) return;
-    int u = 0;
-    while (p >= NV - u) { p -= NV - u; u++; }
-    const int v = u + p;
-    const IpmSizes S = ipm_sizes(C);
-    const double *q = A.q + b * S.q + (size_t)k * NJ;
-    const double *qd = A.qd + b * S.u + (size_t)k * NJ;
-    const double *Fv = A.F + b * S.f + (size_t)k * NFA;
-    const double *tv = A.tau + b * S.u + (size_t)k * NJ;
-    const double *yd = A.yd + b * S.u + (size_t)k * NJ;
-    double cw[NJ], yl[2] = {0.0, 0.0};
-#pragma unroll
-    for (int j = 0; j < NJ; j++) cw[j] = yd[j] + 2.0 * C.wtau * tv[j];
-    for (int l = 0; l < C.nl; l++) yl[l] = A.yl[b * S.l + (size_t)k * C.nl + l];
-    HDual xq[NJ], xqd[NJ], xF[NFA];
-#pragma unroll
-    for (int i = 0; i < NJ; i++) {
-        xq[i] = HDual(q[i], u == i ? 1.0 : 0.0, v == i ? 1.0 : 0.0, 0.0);
-        xqd[i] = HDual(qd[i], u == NJ + i ? 1.0 : 0.0, v == NJ + i ? 1.0 : 0.0, 0.0);
-    }
-#pragma unroll
-    for (int a = 0; a < NFA; a++)
-        xF[a] = HDual(NF > 0 ? Fv[a] : 0.0, u == 2 * NJ + a ? 1.0 : 0.0, v == 2 * NJ + a ? 1.0 : 0.0, 0.0);
-    PhiVis<HDual, NJ> vis;
-    vis.F = &F;
-    vis.cw = cw;
-    vis.yl = yl;
-    vis.nl = C.nl;
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-        HDual acc(0.0);
-        for (int a = 0; a < NF; a++) acc += xF[a] * C.fdir[3 * a + c];
-        vis.Fw[c] = acc;
-    }
-    vis.init();
-    ne_pass<HDual>(M, NJ, xq, xqd, (const HDual *)nullptr, vis);
-    double h2 = vis.phi.d;
-    const double *Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
-    double gn = 0.0;
-#pragma unroll
-    for (int j = 0; j < NJ; j++) gn += Jt[j * NV + u] * Jt[j * NV + v];
-    h2 += 2.0 * C.wtau * gn;
-    if (u == v && u >= NJ && u < 2 * NJ) h2 += 2.0 * C.wqd;
-    if (u == v && u >= 2 * NJ) h2 += 2.0 * C.wF;
-    double *W = A.W + b * S.w + (size_t)k * NV * NV;
-    W[u * NV + v] = h2;
-    W[v * NV + u] = h2;
 }
 
 // ============================================================== init
@@ -196,30 +286,15 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
     const int N = C.N;
     double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *Fv = A.F + b * S.f, *s = A.s + b * S.u;
     const double *q0 = A.q0 + (size_t)b * NJ;
-    auto push = [&](double x, double lo, double hi) {
-        const double k1 = 1e-2, k2 = 1e-2;
-        bool hl = hasb(lo), hh = hasb(hi);
-        if (hl && hh) {
-            double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
-            double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
-            x = fmax(x, lo + pl);
-            x = fmin(x, hi - pu);
-        } else if (hl) {
-            x = fmax(x, lo + k1 * fmax(1.0, fabs(lo)));
-        } else if (hh) {
-            x = fmin(x, hi - k1 * fmax(1.0, fabs(hi)));
-        }
-        return x;
-    };
     for (int e = lane; e < (N + 1) * NJ; e += 64) {
         int k = e / NJ, j = e % NJ;
-        q[e] = (k == 0) ? q0[j] : push(q0[j], C.q_lo[j], C.q_hi[j]);
+        q[e] = (k == 0) ? q0[j] : bound_push(q0[j], C.q_lo[j], C.q_hi[j]);
         A.zqL[b * S.q + e] = (k > 0 && hasb(C.q_lo[j])) ? 1.0 : 0.0;
         A.zqU[b * S.q + e] = (k > 0 && hasb(C.q_hi[j])) ? 1.0 : 0.0;
     }
     for (int e = lane; e < N * NJ; e += 64) {
         int k = e / NJ, j = e % NJ;
-        qd[e] = (k == 0) ? C.qd0[j] : push(0.0, C.qd_lo[j], C.qd_hi[j]);
+        qd[e] = (k == 0) ? C.qd0[j] : bound_push(0.0, C.qd_lo[j], C.qd_hi[j]);
         A.zdL[b * S.u + e] = (k > 0 && hasb(C.qd_lo[j])) ? 1.0 : 0.0;
         A.zdU[b * S.u + e] = (k > 0 && hasb(C.qd_hi[j])) ? 1.0 : 0.0;
         A.vL[b * S.u + e] = hasb(A.tau_lo[e]) ? 1.0 : 0.0;
@@ -231,10 +306,26 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
     for (int e = lane; e < (int)S.l; e += 64) A.yl[b * S.l + e] = 0.0;
     __syncthreads();
     // slacks from tau at the initial point
+    struct SlackOut {
+        double *s;
+        const double *lo, *hi;
+        __device__ void frame(const double *) {}
+        __device__ void force(const double *) {}
+        __device__ void joint(int j, double t, double, double) { s[j] = bound_push(t, lo[j], hi[j]); }
+    };
+    const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
     for (int k = lane; k < N; k += 64) {
-        double tau[NJ], pf[3];
-        node_tau<double, NJ>(M, F, NF, C.fdir, q + (size_t)k * NJ, qd + (size_t)k * NJ, Fv + (size_t)k * NFA, tau, pf);
-        for (int j = 0; j < NJ; j++) s[k * NJ + j] = push(tau[j], A.tau_lo[k * NJ + j], A.tau_hi[k * NJ + j]);
+        double Fw[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            double acc = 0.0;
+#pragma unroll
+            for (int a = 0; a < NF; a++) acc += Fv[(size_t)k * NFA + a] * C.fdir[3 * a + r];
+            Fw[r] = acc;
+        }
+        ArrIn<NJ> in{q + (size_t)k * NJ, qd + (size_t)k * NJ};
+        SlackOut so{s + (size_t)k * NJ, A.tau_lo + (size_t)k * NJ, A.tau_hi + (size_t)k * NJ};
+        node_values<NJ>(M, F, fp, in, Fw, so);
     }
     if (lane == 0) {
         ProbState st;
@@ -246,6 +337,31 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
 }
 
 // ============================================================== one IPM iteration
+// line-search trial point x + alpha dx, read on use by node_values
+struct TrialIn {
+    const double *xq, *dxq, *xqd, *dxqd;
+    double al;
+    __device__ double q(int i) const { return xq[i] + al * dxq[i]; }
+    __device__ double qd(int i) const { return xqd[i] + al * dxqd[i]; }
+};
+// accumulates wtau |tau|^2, |tau - s| on the bounded torque rows and |p - ref| on the line
+struct MeritOut {
+    const double *s, *ds, *tlo, *thi, *lref;
+    double al, wtau, c, th;
+    int nl;
+    bool line;
+    __device__ void frame(const double *p) {
+        if (line)
+            for (int l = 0; l < nl; l++) th += fabs(p[l] - lref[l]);
+    }
+    __device__ void force(const double *) {}
+    __device__ void joint(int j, double t, double, double) {
+        c += wtau * t * t;
+        if (hasb(tlo[j]) || hasb(thi[j])) th += fabs(t - (s[j] + al * ds[j]));
+    }
+};
+
+
 template <int NJ, int NF, int NL>
 __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
@@ -256,7 +372,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     constexpr int MB = 3 * NJ + NF + NL;
     __shared__ DevModel M;
     __shared__ DevFrame F;
-    __shared__ double Dd_s[NJ], rdd_s[NJ];
+    __shared__ double Dd_s[NJ], Ss_s[NJ], rdd_s[NJ];
     __shared__ int perm[MB], piv[MB];
     const int b = blockIdx.x, lane = threadIdx.x;
     if (b >= batch) return;
@@ -350,6 +466,15 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     const double sd = fmax(s_max, (sum_mult + sum_bmult) / fmax(1.0, (double)(n_mult + n_bmult))) / s_max;
     const double sc = fmax(s_max, sum_bmult / fmax(1.0, (double)n_bmult)) / s_max;
     const double E0 = fmax(fmax(dinf / sd, pinf), cinf0 / sc);
+    TRACE(0, dinf); TRACE(1, pinf); TRACE(2, cinf0); TRACE(3, mu);
+#ifdef MF_TRACE
+    {
+        double f = 0.0;
+        for (int k = lane; k < N; k += 64) f += cost[k];
+        f = wave_sum(f);
+        TRACE(14, f);
+    }
+#endif
     double Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
     st.E0 = E0;
     st.cviol = pinf;
@@ -394,6 +519,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
     }
     const double tau_fb = fmax(tau_min, 1.0 - mu);
+    TRACE(4, mu);
     STAMP(0);
 
     // ---------------- barrier Sigma and gradients
@@ -402,8 +528,9 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         double sx = 0, gp = 0;
         if (k > 0) {
             double x = q[e];
-            if (hasb(QLO[j])) { sx += zqL[e] / (x - QLO[j]); gp -= mu / (x - QLO[j]); }
-            if (hasb(QHI[j])) { sx += zqU[e] / (QHI[j] - x); gp += mu / (QHI[j] - x); }
+            sx = sigma_pair(zqL[e], zqU[e], x, QLO[j], QHI[j]);
+            if (hasb(QLO[j])) gp -= mu / (x - QLO[j]);
+            if (hasb(QHI[j])) gp += mu / (QHI[j] - x);
         }
         Sxq[e] = sx; gphq[e] = gp;
     }
@@ -412,12 +539,14 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         double sx = 0, gp = 0, ss = 0, gs = 0;
         if (k > 0) {
             double x = qd[e];
-            if (hasb(DLO[j])) { sx += zdL[e] / (x - DLO[j]); gp -= mu / (x - DLO[j]); }
-            if (hasb(DHI[j])) { sx += zdU[e] / (DHI[j] - x); gp += mu / (DHI[j] - x); }
+            sx = sigma_pair(zdL[e], zdU[e], x, DLO[j], DHI[j]);
+            if (hasb(DLO[j])) gp -= mu / (x - DLO[j]);
+            if (hasb(DHI[j])) gp += mu / (DHI[j] - x);
         }
         double x = s[e];
-        if (hasb(tlo[e])) { ss += vL[e] / (x - tlo[e]); gs -= mu / (x - tlo[e]); }
-        if (hasb(thi[e])) { ss += vU[e] / (thi[e] - x); gs += mu / (thi[e] - x); }
+        ss = sigma_pair(vL[e], vU[e], x, tlo[e], thi[e]);
+        if (hasb(tlo[e])) gs -= mu / (x - tlo[e]);
+        if (hasb(thi[e])) gs += mu / (thi[e] - x);
         Sxd[e] = sx; gphd[e] = gp; Ss[e] = ss; gphs[e] = gs;
     }
     __threadfence_block();
@@ -469,20 +598,19 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
                 if (TACT(k, j)) {
                     double sg = Ss[i] + dw;
                     Dd_s[j] = sg / (1.0 + dc * sg);
+                    Ss_s[j] = Ss[i];
                     rdd_s[j] = (tau[i] - s[i]) + (gphs[i] - yd[i]) / sg;
-                } else { Dd_s[j] = 0.0; rdd_s[j] = 0.0; }
+                } else { Dd_s[j] = 0.0; Ss_s[j] = 0.0; rdd_s[j] = 0.0; }
                 cs[j] = q[k * n + j] + h * qd[k * n + j] - q[(k + 1) * n + j];
             }
             __syncthreads();
+            const bool dreg = (dw != 0.0 || dc != 0.0);
             for (int e = lane; e < NV * NV; e += 64) {
                 int u = e / NV, v = e % NV;
-                double a = Wk[u * NV + v];
-                for (int jj = 0; jj < n; jj++) a += Jtk[jj * NV + u] * Dd_s[jj] * Jtk[jj * NV + v];
-                if (u == v) {
-                    a += dw + (u >= 2 * n ? dFr : 0.0);
-                    if (u < n) a += Sxq[k * n + u];
-                    else if (u < 2 * n) a += Sxd[k * n + u - n];
-                }
+                double a = Wk[u * NV + v];  // H0_k from k_eval_node (Sigma_s, Sigma_x included)
+                if (dreg)
+                    for (int jj = 0; jj < n; jj++) a += Jtk[jj * NV + u] * (Dd_s[jj] - Ss_s[jj]) * Jtk[jj * NV + v];
+                if (u == v) a += dw + (u >= 2 * n ? dFr : 0.0);
                 Hs[e] = a;
             }
             for (int u = lane; u < NV; u += 64) {
@@ -610,6 +738,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     }
     STAMP(2);
     STAMP_COUNT(8, ntries);
+    TRACE(5, dFr); TRACE(6, dw); TRACE(7, dc); TRACE(8, (double)ntries);
     if (!factor_ok) { finish(ST_INERTIA); return; }
     st.reg_tier = tier;
     st.reg_last = reg;
@@ -645,9 +774,14 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         if (k + 1 < N)
             for (int l = lane; l < nl; l += 64) dyl[(k + 1) * nl + l] = ((nl > 0) && LINE_ON(k + 1)) ? us[NU + l] : 0.0;
         __syncthreads();
+        // dyc_k = grad V_{k+1}(dx_{k+1}) + Jl_{k+1}^T dyl_{k+1}: the node-(k+1) line constraint was
+        // pushed back onto stage k, so V_{k+1} does not contain it but the q_{k+1} row of the KKT does
+        const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
         for (int j = lane; j < n; j += 64) {
             double a = wk[NU + NL + j];
             for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * cs[i];
+            if (con1)
+                for (int l = 0; l < nl; l++) a += Jl[((size_t)(k + 1) * nl + l) * n + j] * us[NU + l];
             dyc[k * n + j] = a;
             xs[j] = cs[j];
         }
@@ -658,6 +792,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     __syncthreads();
 
     // ---------------- dyd, ds, dz, dv
+    double pcorr = 0.0;  // sum Sigma_s (ds^2 - (J dx)^2): turns p^T H0 p into the oracle's p^T (W + Sigma) p
     for (int e = lane; e < N * n; e += 64) {
         int k = e / n, j = e % n, i = e;
         if (!TACT(k, j)) { dyd[i] = 0.0; ds[i] = 0.0; continue; }
@@ -669,6 +804,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         double rs = gphs[i] - yd[i], rd = tau[i] - s[i];
         dyd[i] = Dd * (jdx + rd + rs / sg);
         ds[i] = (dyd[i] - rs) / sg;
+        pcorr += Ss[i] * (ds[i] * ds[i] - jdx * jdx);
     }
     for (int e = lane; e < (N + 1) * n; e += 64) {
         int k = e / n, j = e % n;
@@ -720,28 +856,38 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     }
     ap = wave_min(ap);
     az = wave_min(az);
+    TRACE(9, ap); TRACE(10, az);
 
     // ---------------- merit at the current point, directional derivative, curvature
     // merit of a point (x + alpha dx); alpha = 0 uses the stored node values
+    const int fpj = (NF > 0 || NL > 0) ? F.parent : -1;
     auto merit = [&](double alpha, double &phi, double &theta, bool &ok_out) {
         double f = 0, bar = 0, th = 0;
         int bad = 0;
         for (int k = lane; k < N; k += 64) {
-            double tq[NJ], tqd[NJ], tF[NFA], tt[NJ], pf[3];
-            for (int j = 0; j < n; j++) { tq[j] = q[k * n + j] + alpha * dq[k * n + j]; tqd[j] = qd[k * n + j] + alpha * dqd[k * n + j]; }
-            for (int a = 0; a < NFA; a++) tF[a] = NF > 0 ? Fv[k * NFA + a] + alpha * dF[k * NFA + a] : 0.0;
-            node_tau<double, NJ>(M, F, NF, C.fdir, tq, tqd, tF, tt, pf);
-            double c = 0.0;
-            for (int a = 0; a < nf; a++) c += C.wF * tF[a] * tF[a];
-            for (int j = 0; j < n; j++) c += C.wqd * tqd[j] * tqd[j] + C.wtau * tt[j] * tt[j];
-            f += c;
-            for (int j = 0; j < n; j++) {
-                double qn = q[(k + 1) * n + j] + alpha * dq[(k + 1) * n + j];
-                th += fabs(tq[j] + h * tqd[j] - qn);
-                if (TACT(k, j)) th += fabs(tt[j] - (s[k * n + j] + alpha * ds[k * n + j]));
+            double Fw[3], c = 0.0;
+#pragma unroll
+            for (int r = 0; r < 3; r++) Fw[r] = 0.0;
+#pragma unroll
+            for (int a = 0; a < NF; a++) {
+                const double tF = Fv[k * NFA + a] + alpha * dF[k * NFA + a];
+                c += C.wF * tF * tF;
+#pragma unroll
+                for (int r = 0; r < 3; r++) Fw[r] += tF * C.fdir[3 * a + r];
             }
-            if (LINE_ON(k))
-                for (int l = 0; l < nl; l++) th += fabs(pf[l] - lref[l]);
+            TrialIn tin{q + (size_t)k * n, dq + (size_t)k * n, qd + (size_t)k * n, dqd + (size_t)k * n, alpha};
+            MeritOut mo{s + (size_t)k * n, ds + (size_t)k * n, tlo + (size_t)k * n, thi + (size_t)k * n, lref,
+                        alpha, C.wtau, 0.0, 0.0, nl, LINE_ON(k)};
+            node_values<NJ>(M, F, fpj, tin, Fw, mo);
+#pragma unroll
+            for (int j = 0; j < NJ; j++) {
+                const double tq = q[k * n + j] + alpha * dq[k * n + j], tqd = qd[k * n + j] + alpha * dqd[k * n + j];
+                const double qn = q[(k + 1) * n + j] + alpha * dq[(k + 1) * n + j];
+                c += C.wqd * tqd * tqd;
+                th += fabs(tq + h * tqd - qn);
+            }
+            f += c + mo.c;
+            th += mo.th;
         }
         for (int e = n + lane; e < (N + 1) * n; e += 64) {
             int j = e % n;
@@ -766,38 +912,14 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         theta = th;
         ok_out = (bad == 0);
     };
-    // merit at the current point from the node values the eval kernel stored
+    // merit at the current point through the same value sweep as the trial points, so that
+    // m(alpha) - m(0) carries no round-off mismatch between two code paths
     double phi0, th0;
     {
-        double f = 0, bar = 0, th = 0;
-        for (int k = lane; k < N; k += 64) {
-            f += cost[k];
-            for (int j = 0; j < n; j++) {
-                th += fabs(q[k * n + j] + h * qd[k * n + j] - q[(k + 1) * n + j]);
-                if (TACT(k, j)) th += fabs(tau[k * n + j] - s[k * n + j]);
-            }
-            if (LINE_ON(k))
-                for (int l = 0; l < nl; l++) th += fabs(line[k * nl + l]);
-        }
-        for (int e = n + lane; e < (N + 1) * n; e += 64) {
-            int j = e % n;
-            if (hasb(QLO[j])) bar -= log(q[e] - QLO[j]);
-            if (hasb(QHI[j])) bar -= log(QHI[j] - q[e]);
-        }
-        for (int e = lane; e < N * n; e += 64) {
-            int k = e / n, j = e % n;
-            if (k > 0) {
-                if (hasb(DLO[j])) bar -= log(qd[e] - DLO[j]);
-                if (hasb(DHI[j])) bar -= log(DHI[j] - qd[e]);
-            }
-            if (hasb(tlo[e])) bar -= log(s[e] - tlo[e]);
-            if (hasb(thi[e])) bar -= log(thi[e] - s[e]);
-        }
-        f = wave_sum(f); bar = wave_sum(bar); th = wave_sum(th);
-        phi0 = f + mu * bar;
-        th0 = th;
+        bool ok0;
+        merit(0.0, phi0, th0, ok0);
     }
-    double gdot = 0, pHp = 0;
+    double gdot = 0, pHp = pcorr;
     for (int k = lane; k < N; k += 64) {
         const double *Wk = W + (size_t)k * NV * NV;
         double dx[NV];
@@ -808,13 +930,10 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
             for (int v = 0; v < NV; v++) pHp += dx[u] * Wk[u * NV + v] * dx[v];
         }
     }
-    for (int e = lane; e < N * n; e += 64) {
-        gdot += gphd[e] * dqd[e] + gphs[e] * ds[e];
-        pHp += Sxd[e] * dqd[e] * dqd[e] + Ss[e] * ds[e] * ds[e];
-    }
+    for (int e = lane; e < N * n; e += 64) gdot += gphd[e] * dqd[e] + gphs[e] * ds[e];
     for (int e = n + lane; e < (N + 1) * n; e += 64) {
         gdot += gphq[e] * dq[e];
-        pHp += Sxq[e] * dq[e] * dq[e];
+        if (e >= N * n) pHp += Sxq[e] * dq[e] * dq[e];  // q_N (stages k < N carry Sigma_x in H0)
     }
     gdot = wave_sum(gdot);
     pHp = wave_sum(pHp);
@@ -842,6 +961,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     }
     STAMP(5);
     STAMP_COUNT(9, nls);
+    TRACE(11, alpha); TRACE(12, accepted ? 1.0 : 0.0); TRACE(13, nu); TRACE(15, (double)nls);
     if (!accepted) {
         st.n_ls_fail++;
         st.consec_fail++;
@@ -929,18 +1049,15 @@ struct IpmLaunch {
                      hipStream_t s) {
         hipLaunchKernelGGL((k_ipm_init<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
     }
-    // phase 0: node values + Jacobians, 1: Lagrangian Hessians, 2: per-problem IPM step
+    // phase 0: node derivatives (k_eval_node), 1: per-problem IPM step (k_ipm_iter)
     static void iter(int phase, const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A,
                      int batch, hipStream_t s) {
         constexpr int NV = 2 * NJ + NF;
-        constexpr int NP = NV * (NV + 1) / 2;
-        long tj = (long)batch * C.N * NV, th = (long)batch * C.N * NP;
+        constexpr int NPB = 256 / NV;
+        long nodes = (long)batch * C.N;
         if (phase == 0)
-            hipLaunchKernelGGL((k_eval_jac<NJ, NF>), dim3((unsigned)((tj + 255) / 256)), dim3(256), 0, s, M, F, C,
-                               A, batch);
-        else if (phase == 1)
-            hipLaunchKernelGGL((k_eval_hess<NJ, NF>), dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, M, F,
-                               C, A, batch);
+            hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3((unsigned)((nodes + NPB - 1) / NPB)), dim3(256), 0, s,
+                               M, F, C, A, batch);
         else
             hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
     }
@@ -962,7 +1079,7 @@ bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevF
 #define MF_CASE(NJ, NF, NL)                                                       \
     if (n == NJ && nf == NF && nl == NL) {                                        \
         if (what == 0) IpmLaunch<NJ, NF, NL>::init(M, F, C, A, batch, s);          \
-        else if (what >= 10 && what <= 12) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
+        else if (what >= 10 && what <= 11) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
         else IpmLaunch<NJ, NF, NL>::output(C, A, batch, w, status, iters, kkt, obj, s); \
         return true;                                                              \
     }
@@ -974,6 +1091,13 @@ bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevF
 }
 
 }  // namespace mf
+
+#ifdef MF_TRACE
+extern "C" int mf_debug_trace(double *out, int nprob) {
+    if (nprob > 16) nprob = 16;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mf::mf_trace_buf), sizeof(double) * 512 * 16 * nprob) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef MF_PHASE_STAMPS
 extern "C" int mf_debug_phase_stamps(unsigned long long *out, int nprob) {

@@ -37,6 +37,7 @@ struct DevJoint {
     double K[9];     // [axis]x
     double K2[9];    // [axis]x^2
     double m, c[3], Ic[9];
+    double uX[3];    // RX^T tX: R_parent tX = A_i E_i^T uX (reverse-sweep reconstruction, adj.hpp)
     int parent;
     int pad;
 };

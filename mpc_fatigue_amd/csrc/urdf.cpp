@@ -331,4 +331,43 @@ Model build_model_from_urdf(const char *xml) {
     return M;
 }
 
+// Device image of the model: joint placements, Rodrigues matrices K = [a]x and
+// K^2 (R(q) = I + sin q K + (1 - cos q) K^2), inertial parameters.
+DevModel make_dev_model(const Model &M) {
+    DevModel D;
+    memset(&D, 0, sizeof D);
+    D.n = (int)M.joints.size();
+    D.serial = 1;
+    for (int k = 0; k < 3; k++) D.g[k] = M.gravity[k];
+    for (int i = 0; i < D.n; i++) {
+        const Joint &J = M.joints[i];
+        DevJoint &d = D.j[i];
+        memcpy(d.RX, J.R, sizeof d.RX);
+        memcpy(d.tX, J.t, sizeof d.tX);
+        memcpy(d.axis, J.axis, sizeof d.axis);
+        const double *a = J.axis;
+        double K[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
+        memcpy(d.K, K, sizeof K);
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) d.K2[3 * r + c] = K[3 * r] * K[c] + K[3 * r + 1] * K[3 + c] + K[3 * r + 2] * K[6 + c];
+        d.m = J.mass;
+        memcpy(d.c, J.com, sizeof d.c);
+        memcpy(d.Ic, J.Ic, sizeof d.Ic);
+        for (int r = 0; r < 3; r++) d.uX[r] = J.R[r] * J.t[0] + J.R[3 + r] * J.t[1] + J.R[6 + r] * J.t[2];
+        d.parent = J.parent;
+        if (J.parent != i - 1) D.serial = 0;
+    }
+    return D;
+}
+
+DevFrame make_dev_frame(const Model &M, int frame) {
+    DevFrame F;
+    memset(&F, 0, sizeof F);
+    const Frame &f = M.frames[frame];
+    F.parent = f.parent;
+    memcpy(F.R, f.R, sizeof F.R);
+    memcpy(F.t, f.t, sizeof F.t);
+    return F;
+}
+
 }  // namespace mf

@@ -101,16 +101,21 @@ class OCP:
         _lib.check(_lib.lib().mf_solve_batch_dev(self._h, batch, q0_ptr, lref_ptr, C.byref(o), out["w"],
                                                  out["status"], out["iters"], out["kkt"], out["obj"], stream))
 
-    KERNELS = ("k_eval_jac", "k_eval_hess", "k_ipm_iter")
-
     def timing(self, enable: bool = True) -> None:
         _lib.check(_lib.lib().mf_problem_timing(self._h, int(enable)))
 
     def kernel_stats(self) -> dict:
-        ms = np.zeros(3)
-        n = (C.c_long * 3)()
+        """{kernel name: (total ms, launches)} of the solver's launches since timing(True)."""
+        K = _lib.MF_NKERNELS
+        ms = np.zeros(K)
+        n = (C.c_long * K)()
         _lib.check(_lib.lib().mf_problem_kernel_stats(self._h, _lib.dptr(ms), n))
-        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
+        out = {}
+        for i in range(K):
+            name = _lib.lib().mf_kernel_name(i).decode()
+            if name:
+                out[name] = (float(ms[i]), int(n[i]))
+        return out
 
     def node_eval(self, x, u, line_ref=None):
         """(x, u) -> (xnext, g, cost, jac) for a batch of shooting nodes (mf_node_eval)."""

@@ -138,7 +138,10 @@ def test_solve_pilz3_matches_oracle():
 
 
 def test_solve_pilz6_batch_matches_oracle():
-    N, B = 20, 6
+    """C5 instances at N=20: the GPU iteration is the oracle's, so every horizon converges in
+    the same number of iterations (+-1 for round-off at a tie) to the same point (q 1e-7 rad,
+    F 1e-9 N; the -F^2 objective leaves q flat along the line, so q is the looser one)."""
+    N, B = 20, 12
     base = PR.pilz6_bench(N=N)
     ocp = OCP(base)
     ref = load_urdf_file(PR.urdf_path(base["urdf"]))
@@ -147,11 +150,11 @@ def test_solve_pilz6_batch_matches_oracle():
     res = ocp.solve(Q0, line_ref=LR, F_init=PR.BENCH_F_INIT, **SOLVE_OPTS)
     specs = [PR.pilz6_bench(N=N, q0=Q0[b], line_ref=LR[b]) for b in range(B)]
     W, R = O.solve_batch(ref, specs, F_init=PR.BENCH_F_INIT, **SOLVE_OPTS)
-    agree = 0
     for b in range(B):
-        if R[b].status == 0 and res.status[b] == 0:
-            q_gpu, _, _ = ocp.unpack(res.w[b])
-            q_ref, _, _ = ocp.unpack(W[b])
-            if np.abs(q_gpu - q_ref).max() <= 1e-6:
-                agree += 1
-    assert agree >= B - 1, (agree, [r.status for r in R], res.status)
+        assert R[b].status == 0 and res.status[b] == 0, (b, R[b].status, res.status[b])
+        q_gpu, _, F_gpu = ocp.unpack(res.w[b])
+        q_ref, _, F_ref = ocp.unpack(W[b])
+        assert np.abs(q_gpu - q_ref).max() <= 1e-7, (b, np.abs(q_gpu - q_ref).max())
+        assert np.abs(F_gpu - F_ref).max() <= 1e-9, (b, np.abs(F_gpu - F_ref).max())
+        assert abs(int(res.iters[b]) - R[b].iter) <= 1, (b, res.iters[b], R[b].iter)
+        assert abs(res.obj[b] - R[b].obj) <= 1e-9 * abs(R[b].obj)
