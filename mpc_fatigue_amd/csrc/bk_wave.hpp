@@ -46,6 +46,15 @@ __device__ __forceinline__ void wave_argmax(double &v, int &idx) {
     }
 }
 
+// The workgroups that use these routines are exactly one wavefront (64 lanes in lockstep),
+// so ordering LDS traffic only needs the wave's own LDS operations to have completed:
+// s_waitcnt lgkmcnt(0) plus a compiler memory barrier.  __syncthreads() is a workgroup
+// release fence and also waits for vmcnt(0) while global stores are outstanding -- and vmcnt
+// retires in order, so it would drain every register prefetch in flight as well.
+__device__ __forceinline__ void wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// all of the wave's memory operations (global stores read back by other lanes, LDS) complete
+__device__ __forceinline__ void wave_mem_sync() { __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
+
 struct BKInertia {
     int pos, neg, zero;
 };
@@ -60,15 +69,15 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
     __syncthreads();
     int k = 0;
     while (k < m) {
-        double v = 0.0;
-        int idx = m;  // sentinel: no candidate
-        for (int i = k + 1 + lane; i < m; i += 64) {
+        // pivot search: every lane scans the (<= m) candidates itself from LDS broadcast reads --
+        // a serial scan of a short column is far cheaper than a 64-lane shuffle reduction
+        // (ds_bpermute round trips); ties keep the smallest index, like a sequential idamax
+        double colmax = 0.0;
+        int imax = k;
+        for (int i = k + 1; i < m; i++) {
             double a = fabs(A[i * LD + k]);
-            if (a > v || (a == v && idx == m)) { v = a; idx = i; }
+            if (a > colmax) { colmax = a; imax = i; }
         }
-        wave_argmax(v, idx);
-        double colmax = v;
-        int imax = (idx == m) ? k : idx;
         double absakk = fabs(A[k * LD + k]);
         int kstep = 1, kp = k;
         if (fmax(absakk, colmax) == 0.0) {
@@ -81,10 +90,9 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
         if (absakk >= alpha * colmax) {
             kp = k;
         } else {
-            double rv = 0.0;
-            for (int j = k + lane; j < m; j += 64)
-                if (j != imax) rv = fmax(rv, fabs(A[imax * LD + j]));
-            double rowmax = wave_max(rv);
+            double rowmax = 0.0;
+            for (int j = k; j < m; j++)
+                if (j != imax) rowmax = fmax(rowmax, fabs(A[imax * LD + j]));
             if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
             else if (fabs(A[imax * LD + imax]) >= alpha * rowmax) kp = imax;
             else { kp = imax; kstep = 2; }
@@ -156,6 +164,288 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
     }
     __syncthreads();
     return in;
+}
+
+// Same factorisation with a compile-time size M <= 64: the pivot scans are unrolled, so their
+// LDS reads issue back to back instead of one dependent round trip per candidate.
+template <int LD, int M>
+__device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
+    const int lane = threadIdx.x;
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    BKInertia in{0, 0, 0};
+    if (lane < M) perm[lane] = lane;
+    wave_lds_sync();
+    int k = 0;
+    while (k < M) {
+        double cv[M];
+#pragma unroll
+        for (int i = 0; i < M; i++) cv[i] = A[i * LD + k];
+        double colmax = 0.0;
+        int imax = k;
+#pragma unroll
+        for (int i = 1; i < M; i++) {
+            const double a = (i > k) ? fabs(cv[i]) : 0.0;
+            if (a > colmax) { colmax = a; imax = i; }
+        }
+        double absakk = 0.0;
+#pragma unroll
+        for (int i = 0; i < M; i++)
+            if (i == k) absakk = fabs(cv[i]);
+        int kstep = 1, kp = k;
+        if (fmax(absakk, colmax) == 0.0) {
+            in.zero++;
+            if (lane == 0) piv[k] = 1;
+            k++;
+            wave_lds_sync();
+            continue;
+        }
+        if (absakk >= alpha * colmax) {
+            kp = k;
+        } else {
+            double rv[M];
+#pragma unroll
+            for (int j = 0; j < M; j++) rv[j] = A[imax * LD + j];
+            double rowmax = 0.0, aii = 0.0;
+#pragma unroll
+            for (int j = 0; j < M; j++) {
+                if (j >= k && j != imax) rowmax = fmax(rowmax, fabs(rv[j]));
+                if (j == imax) aii = fabs(rv[j]);
+            }
+            if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
+            else if (aii >= alpha * rowmax) kp = imax;
+            else { kp = imax; kstep = 2; }
+        }
+        int kk = k + kstep - 1;
+        if (kp != kk) {
+            wave_lds_sync();
+            for (int j = lane; j < M; j += 64) {
+                double t = A[kk * LD + j]; A[kk * LD + j] = A[kp * LD + j]; A[kp * LD + j] = t;
+            }
+            wave_lds_sync();
+            for (int i = lane; i < M; i += 64) {
+                double t = A[i * LD + kk]; A[i * LD + kk] = A[i * LD + kp]; A[i * LD + kp] = t;
+            }
+            if (lane == 0) { int t = perm[kk]; perm[kk] = perm[kp]; perm[kp] = t; }
+            wave_lds_sync();
+        }
+        if (kstep == 1) {
+            const double d = A[k * LD + k];
+            if (d > 0) in.pos++; else if (d < 0) in.neg++; else in.zero++;
+            const double inv = 1.0 / d;
+            const int t = M - k - 1;
+            for (int e = lane; e < t * t; e += 64) {
+                const int i = k + 1 + e / t, j = k + 1 + e % t;
+                if (j <= i) {
+                    const double ci = A[i * LD + k], cj = A[j * LD + k];
+                    const double val = A[i * LD + j] - (ci * inv) * cj;
+                    A[i * LD + j] = val;
+                    A[j * LD + i] = val;
+                }
+            }
+            wave_lds_sync();
+            for (int i = k + 1 + lane; i < M; i += 64) {
+                const double l = A[i * LD + k] * inv;
+                A[i * LD + k] = l;
+                A[k * LD + i] = l;
+            }
+            if (lane == 0) piv[k] = 1;
+        } else {
+            const double a = A[k * LD + k], bb = A[(k + 1) * LD + k], c = A[(k + 1) * LD + k + 1];
+            const double det = a * c - bb * bb;
+            if (det < 0) { in.pos++; in.neg++; }
+            else if (det > 0) { if (a + c > 0) in.pos += 2; else in.neg += 2; }
+            else in.zero += 2;
+            const double ia = c / det, ib = -bb / det, ic = a / det;
+            const int t = M - k - 2;
+            for (int e = lane; e < t * t; e += 64) {
+                const int i = k + 2 + e / t, j = k + 2 + e % t;
+                if (j <= i) {
+                    const double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
+                    const double c0j = A[j * LD + k], c1j = A[j * LD + k + 1];
+                    const double l0 = c0i * ia + c1i * ib, l1 = c0i * ib + c1i * ic;
+                    const double val = A[i * LD + j] - (l0 * c0j + l1 * c1j);
+                    A[i * LD + j] = val;
+                    A[j * LD + i] = val;
+                }
+            }
+            wave_lds_sync();
+            for (int i = k + 2 + lane; i < M; i += 64) {
+                const double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
+                A[i * LD + k] = c0i * ia + c1i * ib;
+                A[i * LD + k + 1] = c0i * ib + c1i * ic;
+            }
+            if (lane == 0) { piv[k] = 2; piv[k + 1] = 0; }
+        }
+        wave_lds_sync();
+        k += kstep;
+    }
+    return in;
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// Fast path for the stage block K = [[Q, D^T], [D, -dc]] (M = MU + ML, ML <= 2) in registers.
+// Lane i keeps row i of K (symmetric) and row i of the right-hand sides B (M x NR in LDS,
+// nr <= NR columns).  Q is eliminated by LDL^T with 1x1 pivots in natural order, each pivot
+// accepted by the Bunch-Kaufman test |q_kk| >= alpha * max_{i>k} |q_ik| taken within Q; the
+// pivot row is read with v_readlane and the forward substitution is fused into the
+// elimination.  What is left in rows MU.. is the Schur complement S = -dc - D Q^{-1} D^T,
+// solved as one (ML x ML) block.  By Haynsworth additivity inertia(K) = inertia(Q) +
+// inertia(S), so the inertia test is the same exact test as a pivoted factorisation of K.
+// On success the solution overwrites B; if a pivot fails the test (or S is singular) it
+// returns false with A and B untouched and the caller runs the pivoted LDS path.
+template <int LD, int NR, int MU, int ML>
+__device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in) {
+    constexpr int M = MU + ML;
+    static_assert(ML <= 2, "Schur block of at most 2 rows");
+    const int lane = threadIdx.x;
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    double a[M], y[NR];
+#pragma unroll
+    for (int j = 0; j < M; j++) a[j] = (lane < M) ? A[lane * LD + j] : 0.0;
+#pragma unroll
+    for (int c = 0; c < NR; c++) y[c] = (lane < M && c < nr) ? B[lane * NR + c] : 0.0;
+    int pos = 0, neg = 0;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < MU; k++) {
+        if (ok) {
+            double colmax = 0.0;
+#pragma unroll
+            for (int i = k + 1; i < MU; i++) colmax = fmax(colmax, fabs(readlane_d(a[k], i)));
+            const double d = readlane_d(a[k], k);
+            if (!(fabs(d) >= alpha * colmax) || d == 0.0) {
+                ok = false;
+            } else {
+                if (d > 0) pos++; else neg++;
+                const double inv = 1.0 / d;
+                double r[M], yk[NR];
+#pragma unroll
+                for (int j = k + 1; j < M; j++) r[j] = readlane_d(a[j], k);
+#pragma unroll
+                for (int c = 0; c < NR; c++) yk[c] = readlane_d(y[c], k);
+                if (lane > k && lane < M) {
+                    const double l = a[k] * inv;
+#pragma unroll
+                    for (int j = k + 1; j < M; j++) a[j] = a[j] - l * r[j];
+                    a[k] = l;
+#pragma unroll
+                    for (int c = 0; c < NR; c++) y[c] -= l * yk[c];
+                }
+            }
+        }
+    }
+    if (!ok) return false;
+    // Schur block: inertia and x_S = S^{-1} y_S (rows MU..M-1)
+    if (ML == 1) {
+        const double s00 = readlane_d(a[MU], MU);
+        if (s00 == 0.0) return false;
+        if (s00 > 0) pos++; else neg++;
+        if (lane == MU)
+#pragma unroll
+            for (int c = 0; c < NR; c++) y[c] = y[c] / s00;
+    } else if (ML == 2) {
+        const double s00 = readlane_d(a[MU], MU), s01 = readlane_d(a[MU + 1], MU), s11 = readlane_d(a[M - 1], M - 1);
+        const double det = s00 * s11 - s01 * s01;
+        if (det == 0.0) return false;
+        if (det < 0) { pos++; neg++; }
+        else if (s00 + s11 > 0) pos += 2;
+        else neg += 2;
+        double y0[NR], y1[NR];
+#pragma unroll
+        for (int c = 0; c < NR; c++) { y0[c] = readlane_d(y[c], MU); y1[c] = readlane_d(y[c], M - 1); }
+        if (lane == MU)
+#pragma unroll
+            for (int c = 0; c < NR; c++) y[c] = (s11 * y0[c] - s01 * y1[c]) / det;
+        if (lane == M - 1)
+#pragma unroll
+            for (int c = 0; c < NR; c++) y[c] = (s00 * y1[c] - s01 * y0[c]) / det;
+    }
+    // D^{-1} on the Q rows, then L^T x = y from the last row up; lane t (< MU) keeps the unscaled
+    // column t of the eliminated matrix in a[t+1..], so L_it = a[i] / d_t
+    double dinv = 0.0;
+#pragma unroll
+    for (int j = 0; j < MU; j++)
+        if (j == lane) dinv = 1.0 / a[j];
+    if (lane < MU)
+#pragma unroll
+        for (int c = 0; c < NR; c++) y[c] *= dinv;
+#pragma unroll
+    for (int i = M - 1; i > 0; i--) {
+        double xi[NR];
+#pragma unroll
+        for (int c = 0; c < NR; c++) xi[c] = readlane_d(y[c], i);
+        if (lane < i && lane < MU) {
+            const double lit = a[i] * dinv;
+#pragma unroll
+            for (int c = 0; c < NR; c++) y[c] -= lit * xi[c];
+        }
+    }
+    if (lane < M)
+#pragma unroll
+        for (int c = 0; c < NR; c++)
+            if (c < nr) B[lane * NR + c] = y[c];
+    wave_lds_sync();
+    in.pos = pos;
+    in.neg = neg;
+    in.zero = 0;
+    return true;
+}
+
+// Solve A X = B for nr <= 64 right-hand sides with a compile-time size M: lane c owns column c
+// of B (m x NR row-major in LDS) in registers and runs both triangular sweeps itself, reading
+// the factor by LDS broadcast; no cross-lane traffic and a single barrier.  The L column t
+// acts on rows >= t + 1, or >= t + 2 when t opens a 2x2 pivot (its partner row belongs to D).
+template <int LD, int NR, int M>
+__device__ void bk_solve_cols(const double *A, const int *perm, const int *piv, double *B, int nr) {
+    const int c = threadIdx.x;
+    double y[M];
+    int pv[M];
+    if (c < nr) {
+#pragma unroll
+        for (int i = 0; i < M; i++) {
+            pv[i] = piv[i];
+            y[i] = B[perm[i] * NR + c];
+        }
+#pragma unroll
+        for (int t = 0; t < M; t++) {
+            const int start = t + 1 + (pv[t] == 2 ? 1 : 0);
+#pragma unroll
+            for (int i = t + 1; i < M; i++)
+                if (i >= start) y[i] -= A[i * LD + t] * y[t];
+        }
+#pragma unroll
+        for (int i = 0; i < M; i++) {
+            if (pv[i] == 1) {
+                y[i] = y[i] / A[i * LD + i];
+            } else if (pv[i] == 2 && i + 1 < M) {
+                const double a = A[i * LD + i], bb = A[(i + 1) * LD + i], cc = A[(i + 1) * LD + i + 1];
+                const double det = a * cc - bb * bb;
+                const double y0 = y[i], y1 = y[i + 1];
+                y[i] = (cc * y0 - bb * y1) / det;
+                y[i + 1] = (a * y1 - bb * y0) / det;
+            }
+        }
+#pragma unroll
+        for (int t = M - 1; t >= 0; t--) {
+            const int start = t + 1 + (pv[t] == 2 ? 1 : 0);
+            double acc = y[t];
+#pragma unroll
+            for (int i = t + 1; i < M; i++)
+                if (i >= start) acc -= A[i * LD + t] * y[i];
+            y[t] = acc;
+        }
+    }
+    wave_lds_sync();  // every lane has read the factor and B before B is overwritten
+    if (c < nr) {
+#pragma unroll
+        for (int i = 0; i < M; i++) B[perm[i] * NR + c] = y[i];
+    }
+    wave_lds_sync();
 }
 
 // Solve A X = B for nr right-hand sides; B is m x NR (row-major, LD NR) in LDS.

@@ -35,19 +35,29 @@ __device__ __forceinline__ double sigma_pair(double zL, double zU, double x, dou
 // Diagnostic build only (-DMF_PHASE_STAMPS): per-phase cycle counts of k_ipm_iter,
 // accumulated by lane 0 into a debug buffer (never read by the solver).
 #ifdef MF_PHASE_STAMPS
-__device__ unsigned long long mf_stamp_buf[16 * 4096];
+__device__ unsigned long long mf_stamp_buf[32 * 4096];
+// accumulated in registers (a global read-modify-write per stamp would wait, vmcnt being in
+// order, for every prefetch in flight) and added to the buffer once per launch
 #define STAMP(slot)                                                                   \
     do {                                                                              \
         unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
-        if (lane == 0 && b < 4096) mf_stamp_buf[b * 16 + (slot)] += t_ - t_prev_;     \
+        stamp_acc_[slot] += t_ - t_prev_;                                             \
         t_prev_ = t_;                                                                 \
     } while (0)
-#define STAMP_INIT unsigned long long t_prev_ = __builtin_amdgcn_s_memtime()
-#define STAMP_COUNT(slot, v) do { if (lane == 0 && b < 4096) mf_stamp_buf[b * 16 + (slot)] += (v); } while (0)
+#define STAMP_INIT                                                                    \
+    unsigned long long stamp_acc_[32] = {0};                                          \
+    unsigned long long t_prev_ = __builtin_amdgcn_s_memtime()
+#define STAMP_COUNT(slot, v) do { stamp_acc_[slot] += (v); } while (0)
+#define STAMP_FLUSH                                                                   \
+    do {                                                                              \
+        if (lane == 0 && b < 4096)                                                    \
+            for (int s_ = 0; s_ < 32; s_++) mf_stamp_buf[b * 32 + s_] += stamp_acc_[s_]; \
+    } while (0)
 #else
 #define STAMP(slot) do {} while (0)
 #define STAMP_INIT do {} while (0)
 #define STAMP_COUNT(slot, v) do {} while (0)
+#define STAMP_FLUSH do {} while (0)
 #endif
 
 // IPOPT bound_push / bound_frac = 1e-2: move an initial value strictly inside its bounds
@@ -479,6 +489,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     st.E0 = E0;
     st.cviol = pinf;
     auto finish = [&](int status) {
+        STAMP_FLUSH;
         double f = 0.0;
         for (int k = lane; k < N; k += 64) f += cost[k];
         f = wave_sum(f);
@@ -561,16 +572,76 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     // (n_primal, n_dual) iff every stage block has inertia (NU, NL) (Sylvester),
     // which is the test the oracle's block LDL^T of the whole KKT performs.  Stage 0 has x, qd
     // fixed: only dF_0 with Hessian H_FF.  Slot k of G / wv keeps Ku, Kl, P_{k+1} / ku, kl, p_{k+1}.
+    //
+    // Latency layout: everything a stage needs that does not depend on the recursion (the
+    // gradient g_k, c_k, e_k = line_{k+1} + Jl_{k+1} c_k) is computed for all stages at once by
+    // the whole wave into LDS; the stage Hessian H0_k and Jl_{k+1} are prefetched into registers
+    // one stage ahead, so the serial chain itself issues no dependent global load.
     constexpr int NU = NJ + NF;
     constexpr int NK = NU + NL;
     constexpr int LDK = NK + 1;
     constexpr int NRK = NJ + 1;
     constexpr int NLA2 = NL > 0 ? NL : 1;
-    __shared__ double Hs[NV * NV], gs[NV];
-    __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], cs[NJ], Pn[NJ * NJ];
+    constexpr int NVV = NV * NV;
+    constexpr int NHR = (NVV + 63) / 64;     // H entries per lane
+    constexpr int SLOT = MB * NJ + MB;       // Riccati slot (G_k | wv_k) doubles
+    constexpr int NSR = (SLOT + 63) / 64;
+    __shared__ double Hs[NVV];
+    __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], Pn[NJ * NJ];
     __shared__ double Ks[NK * LDK], Rk[NK * NRK], Yk[NK * NRK];
-    __shared__ double Gl[NLA2 * NJ], el[NLA2];
-    __shared__ double xs[NJ], us[NU + NLA2];
+    __shared__ double Gl[NLA2 * NJ];
+    __shared__ double xs[NJ], us[NU + NLA2], cs[NJ];
+    __shared__ double Sl[SLOT];
+    __shared__ double Jl_s[NJ * NV];  // J_k (torque Jacobian) of the stage, regularised tries only
+    extern __shared__ double dyn_lds[];
+    double *gst = dyn_lds;                    // N x NV   stage gradients g_k
+    double *cst = gst + (size_t)N * NV;       // N x NJ   c_k = q_k + h qd_k - q_{k+1}
+    double *est = cst + (size_t)N * NJ;       // N x NLA2 e_k = line_{k+1} + Jl_{k+1} c_k
+    double *wst = est + (size_t)N * NLA2;     // N x NJ   y_tau + D_tau r_tau (torque rows)
+    double *dst = wst + (size_t)N * NJ;       // N x NJ   D_tau(dw, dc) - Sigma_s (0 unless dw, dc != 0)
+    // g_k for all stages at the current (dw, dc): exactly the primal rows of the KKT right-hand side
+    auto prep_stages = [&](double dwv, double dcv) {
+        for (int e = lane; e < N * n; e += 64) {
+            const int k = e / n, j = e % n;
+            double wv_ = yd[e], dD = 0.0;
+            if (TACT(k, j)) {
+                const double sg = Ss[e] + dwv;
+                const double Dd = sg / (1.0 + dcv * sg);
+                wv_ += Dd * ((tau[e] - s[e]) + (gphs[e] - yd[e]) / sg);
+                dD = Dd - Ss[e];
+            }
+            wst[e] = wv_;
+            dst[e] = dD;
+            cst[e] = q[e] + h * qd[e] - q[e + n];
+        }
+        wave_lds_sync();
+        for (int e = lane; e < N * NV; e += 64) {
+            const int k = e / NV, u = e % NV;
+            double g = gf[e];
+            const double *Jtk = Jt + (size_t)k * n * NV;
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) g += Jtk[jj * NV + u] * wst[k * n + jj];
+            if (u < n) {
+                g += gphq[k * n + u] + yc[k * n + u] - (k > 0 ? yc[(k - 1) * n + u] : 0.0);
+#pragma unroll
+                for (int l = 0; l < NL; l++) g += Jl[(k * nl + l) * n + u] * yl[k * nl + l];
+            } else if (u < 2 * n) {
+                g += gphd[k * n + u - n] + h * yc[k * n + u - n];
+            }
+            gst[e] = g;
+        }
+        for (int e = lane; e < N * nl; e += 64) {
+            const int k = e / nl, l = e % nl;
+            double a = 0.0;
+            if (LINE_ON(k + 1) && k + 1 <= N - 1) {
+                a = line[(k + 1) * nl + l];
+#pragma unroll
+                for (int i = 0; i < NJ; i++) a += Jl[((size_t)(k + 1) * nl + l) * n + i] * cst[k * n + i];
+            }
+            est[k * NLA2 + l] = a;
+        }
+        wave_lds_sync();
+    };
     double dw = 0.0, dc = 0.0, dFr = 0.0;
     const int reg_tier0 = st.reg_tier;
     const double reg_last0 = st.reg_last;
@@ -580,97 +651,126 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     if (tier == 1) dFr = reg; else if (tier == 2) dw = reg;
     bool factor_ok = false;
     int ntries = 0;
+    double prep_dw = NAN, prep_dc = NAN;
     for (int tries = 0; tries < 60; tries++) {
         ntries++;
         bool ok = true, zero = false;
+        if (!(dw == prep_dw && dc == prep_dc)) {
+            prep_stages(dw, dc);
+            prep_dw = dw;
+            prep_dc = dc;
+        }
+        const bool dreg = (dw != 0.0 || dc != 0.0);
         // terminal value function V_N = 1/2 x^T P x + p^T x
         for (int e = lane; e < n * n; e += 64) {
             int i = e / n, j = e % n;
             Ps[e] = (i == j) ? Sxq[N * n + i] + dw : 0.0;
         }
         for (int j = lane; j < n; j += 64) ps[j] = gphq[N * n + j] - yc[(N - 1) * n + j];
-        __syncthreads();
+        // prefetch H0_{N-1} (and J_{N-1} when the torque block is regularised)
+        constexpr int NJV = NJ * NV, NJR = (NJV + 63) / 64;
+        double hr[NHR], jr[NJR];
+#pragma unroll
+        for (int t = 0; t < NHR; t++) {
+            const int e = lane + 64 * t;
+            hr[t] = (e < NVV) ? W[(size_t)(N - 1) * NVV + e] : 0.0;
+        }
+#pragma unroll
+        for (int t = 0; t < NJR; t++) {
+            const int e = lane + 64 * t;
+            jr[t] = (dreg && e < NJV) ? Jt[(size_t)(N - 1) * NJV + e] : 0.0;
+        }
+        double glr = 0.0;  // Jl_{k+1} entry of this lane for the next stage
+        wave_lds_sync();
         for (int k = N - 1; k >= 0; k--) {
-            const double *Wk = W + (size_t)k * NV * NV, *Jtk = Jt + (size_t)k * n * NV;
-            // ---- stage Hessian H (NV x NV) and gradient g, exactly the primal rows of the KKT
-            for (int j = lane; j < n; j += 64) {
-                int i = k * n + j;
-                if (TACT(k, j)) {
-                    double sg = Ss[i] + dw;
-                    Dd_s[j] = sg / (1.0 + dc * sg);
-                    Ss_s[j] = Ss[i];
-                    rdd_s[j] = (tau[i] - s[i]) + (gphs[i] - yd[i]) / sg;
-                } else { Dd_s[j] = 0.0; Ss_s[j] = 0.0; rdd_s[j] = 0.0; }
-                cs[j] = q[k * n + j] + h * qd[k * n + j] - q[(k + 1) * n + j];
-            }
-            __syncthreads();
-            const bool dreg = (dw != 0.0 || dc != 0.0);
-            for (int e = lane; e < NV * NV; e += 64) {
-                int u = e / NV, v = e % NV;
-                double a = Wk[u * NV + v];  // H0_k from k_eval_node (Sigma_s, Sigma_x included)
-                if (dreg)
-                    for (int jj = 0; jj < n; jj++) a += Jtk[jj * NV + u] * (Dd_s[jj] - Ss_s[jj]) * Jtk[jj * NV + v];
-                if (u == v) a += dw + (u >= 2 * n ? dFr : 0.0);
-                Hs[e] = a;
-            }
-            for (int u = lane; u < NV; u += 64) {
-                double g = gf[k * NV + u];
-                for (int jj = 0; jj < n; jj++) g += Jtk[jj * NV + u] * (yd[k * n + jj] + Dd_s[jj] * rdd_s[jj]);
-                if (u < n) {
-                    g += gphq[k * n + u] + yc[k * n + u] - (k > 0 ? yc[(k - 1) * n + u] : 0.0);
-                    for (int l = 0; l < nl; l++) g += Jl[(k * nl + l) * n + u] * yl[k * nl + l];
-                } else if (u < 2 * n) {
-                    g += gphd[k * n + u - n] + h * yc[k * n + u - n];
+            // ---- H_k = H0_k (+ regularisation) into LDS; prefetch H0_{k-1}, Jl_k (, J_{k-1})
+            if (dreg) {
+#pragma unroll
+                for (int t = 0; t < NJR; t++) {
+                    const int e = lane + 64 * t;
+                    if (e < NJV) Jl_s[e] = jr[t];
                 }
-                gs[u] = g;
+                wave_lds_sync();
+            }
+            const double *dDk = dst + (size_t)k * n;
+#pragma unroll
+            for (int t = 0; t < NHR; t++) {
+                const int e = lane + 64 * t;
+                if (e < NVV) {
+                    const int u = e / NV, v = e % NV;
+                    double a = hr[t];
+                    if (dreg)
+#pragma unroll
+                        for (int jj = 0; jj < NJ; jj++) a += Jl_s[jj * NV + u] * dDk[jj] * Jl_s[jj * NV + v];
+                    if (u == v) a += dw + (u >= 2 * n ? dFr : 0.0);
+                    Hs[e] = a;
+                }
+            }
+            if (lane < nl * n) Gl[lane] = glr;
+            STAMP(7);
+            if (k > 0) {
+#pragma unroll
+                for (int t = 0; t < NHR; t++) {
+                    const int e = lane + 64 * t;
+                    hr[t] = (e < NVV) ? W[(size_t)(k - 1) * NVV + e] : 0.0;
+                }
+                glr = (lane < nl * n) ? Jl[(size_t)k * nl * n + lane] : 0.0;
+                if (dreg)
+#pragma unroll
+                    for (int t = 0; t < NJR; t++) {
+                        const int e = lane + 64 * t;
+                        jr[t] = (e < NJV) ? Jt[(size_t)(k - 1) * NJV + e] : 0.0;
+                    }
             }
             // s = P c + p ; keep P_{k+1}, p_{k+1} for the forward sweep
             double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
-            for (int j = lane; j < n; j += 64) {
+            const double *ck = cst + (size_t)k * n;
+            if (lane < n) {
+                const int j = lane;
                 double a = ps[j];
-                for (int i = 0; i < n; i++) a += Ps[j * n + i] * cs[i];
+#pragma unroll
+                for (int i = 0; i < NJ; i++) a += Ps[j * n + i] * ck[i];
                 ss[j] = a;
                 wk[NU + NL + j] = ps[j];
             }
             for (int e = lane; e < n * n; e += 64) Gk[(NU + NL) * n + e] = Ps[e];
-            __syncthreads();
+            wave_lds_sync();
+            STAMP(11);
+            const double *gsk = gst + (size_t)k * NV;
             if (k == 0) {
                 // only dF_0 is free (q_0, qd_0 fixed; the stage-1 line constraint is masked)
                 if (nf > 0) {
                     for (int e = lane; e < nf * nf; e += 64) Ks[(e / nf) * LDK + e % nf] = Hs[(2 * n + e / nf) * NV + 2 * n + e % nf];
-                    for (int a = lane; a < nf; a += 64) Rk[a * NRK] = -gs[2 * n + a];
-                    __syncthreads();
-                    BKInertia in = bk_factor_wave<LDK>(Ks, nf, perm, piv);
+                    for (int a = lane; a < nf; a += 64) Rk[a * NRK] = -gsk[2 * n + a];
+                    wave_lds_sync();
+                    BKInertia in = bk_factor_fixed<LDK, NFA>(Ks, perm, piv);
                     if (in.zero) { ok = false; zero = true; break; }
                     if (in.pos != nf) { ok = false; break; }
-                    bk_solve_wave<LDK, NRK>(Ks, nf, perm, piv, Rk, 1, Yk);
+                    bk_solve_cols<LDK, NRK, NFA>(Ks, perm, piv, Rk, 1);
                     for (int a = lane; a < nf; a += 64) wk[NJ + a] = Rk[a * NRK];  // dF_0 (ku slot)
                 }
-                __syncthreads();
+                wave_lds_sync();
                 break;
             }
             const bool con = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
-            if (con) {
-                const double *Jl1 = Jl + (size_t)(k + 1) * nl * n;
-                for (int e = lane; e < nl * n; e += 64) Gl[e] = Jl1[e];
-                for (int l = lane; l < nl; l += 64) {
-                    double a = line[(k + 1) * nl + l];
-                    for (int i = 0; i < n; i++) a += Jl1[l * n + i] * cs[i];
-                    el[l] = a;
-                }
-                __syncthreads();
-            }
+            const double *elk = est + (size_t)k * NLA2;
             // ---- stage block [[Quu, Du^T], [Du, -dc]] and right-hand sides -[Qux | qu ; G | e]
+            // Block rows order the controls as (F, qd): with active torque bounds the force
+            // carries the large curvature Sigma_s (J^T F)^2 and the joint velocities couple to it
+            // weakly, so natural-order 1x1 pivots pass the Bunch-Kaufman test (ldl_schur_regs).
+            // uo(a): control index (qd 0..n-1, F n..) of block row a < NU.
+            auto uo = [&](int a) { return a < NF ? NJ + a : a - NF; };
             for (int e = lane; e < NK * NK; e += 64) {
                 int a = e / NK, c = e % NK;
                 double val;
                 if (a < NU && c < NU) {
-                    val = Hs[(n + a) * NV + n + c];
-                    if (a < n && c < n) val += h * h * Ps[a * n + c];
+                    const int ua = uo(a), uc = uo(c);
+                    val = Hs[(n + ua) * NV + n + uc];
+                    if (ua < n && uc < n) val += h * h * Ps[ua * n + uc];
                 } else if (a >= NU && c >= NU) {
                     val = (a == c) ? (con ? -dc : -1.0) : 0.0;
                 } else {
-                    int l = (a >= NU) ? a - NU : c - NU, v = (a >= NU) ? c : a;
+                    int l = (a >= NU) ? a - NU : c - NU, v = uo((a >= NU) ? c : a);
                     val = (con && v < n) ? h * Gl[l * n + v] : 0.0;
                 }
                 Ks[a * LDK + c] = val;
@@ -679,24 +779,39 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
                 int a = e / NRK, c = e % NRK;
                 double val;
                 if (a < NU) {
-                    if (c < n) val = -(Hs[(n + a) * NV + c] + (a < n ? h * Ps[a * n + c] : 0.0));
-                    else val = -(gs[n + a] + (a < n ? h * ss[a] : 0.0));
+                    const int ua = uo(a);
+                    if (c < n) val = -(Hs[(n + ua) * NV + c] + (ua < n ? h * Ps[ua * n + c] : 0.0));
+                    else val = -(gsk[n + ua] + (ua < n ? h * ss[ua] : 0.0));
                 } else {
                     int l = a - NU;
-                    val = con ? -(c < n ? Gl[l * n + c] : el[l]) : 0.0;
+                    val = con ? -(c < n ? Gl[l * n + c] : elk[l]) : 0.0;
                 }
                 Rk[e] = val;
             }
-            __syncthreads();
-            BKInertia in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
-            if (in.zero) { ok = false; zero = true; break; }
-            if (in.pos != NU || in.neg != NL) { ok = false; break; }
-            bk_solve_wave<LDK, NRK>(Ks, NK, perm, piv, Rk, NRK, Yk);
-            // ---- P_k = Qxx + Qxu Ku + G^T Kl ; p_k = qx + Qxu ku + G^T kl
+            wave_lds_sync();
+            STAMP(12);
+            BKInertia in;
+            const bool fast = ldl_schur_regs<LDK, NRK, NU, NL>(Ks, Rk, NRK, in);
+            STAMP(13);
+            STAMP_COUNT(16, fast ? 0 : 1);
+            STAMP_COUNT(17, 1);
+            if (fast) {
+                if (in.pos != NU || in.neg != NL) { ok = false; break; }
+            } else {
+                in = bk_factor_fixed<LDK, NK>(Ks, perm, piv);
+                if (in.zero) { ok = false; zero = true; break; }
+                if (in.pos != NU || in.neg != NL) { ok = false; break; }
+                bk_solve_cols<LDK, NRK, NK>(Ks, perm, piv, Rk, NRK);
+            }
+            STAMP(14);
+            // ---- P_k = Qxx + Qxu Ku + G^T Kl ; p_k = qx + Qxu ku + G^T kl   (block row a <-> control uo(a))
             for (int e = lane; e < n * n; e += 64) {
                 int i = e / n, j = e % n;
                 double a = Hs[i * NV + j] + Ps[i * n + j];
-                for (int c = 0; c < NU; c++) a += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[c * NRK + j];
+                for (int r = 0; r < NU; r++) {
+                    const int c = uo(r);
+                    a += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[r * NRK + j];
+                }
                 if (con)
                     for (int l = 0; l < nl; l++) a += Gl[l * n + i] * Rk[(NU + l) * NRK + j];
                 Pn[e] = a;
@@ -704,20 +819,26 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
             double pnew = 0.0;
             if (lane < n) {
                 int i = lane;
-                pnew = gs[i] + ss[i];
-                for (int c = 0; c < NU; c++) pnew += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[c * NRK + n];
+                pnew = gsk[i] + ss[i];
+                for (int r = 0; r < NU; r++) {
+                    const int c = uo(r);
+                    pnew += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[r * NRK + n];
+                }
                 if (con)
                     for (int l = 0; l < nl; l++) pnew += Gl[l * n + i] * Rk[(NU + l) * NRK + n];
             }
-            for (int e = lane; e < NK * n; e += 64) Gk[e] = Rk[(e / n) * NRK + e % n];  // Ku (NU x n), Kl (NL x n)
-            for (int a = lane; a < NK; a += 64) wk[a] = Rk[a * NRK + n];              // ku, kl
-            __syncthreads();
+            // slot rows in control order (qd 0..n-1, F, then the NL line multipliers)
+            auto brow = [&](int c) { return c < NU ? (c < NJ ? NF + c : c - NJ) : c; };
+            for (int e = lane; e < NK * n; e += 64) Gk[e] = Rk[brow(e / n) * NRK + e % n];  // Ku (NU x n), Kl (NL x n)
+            for (int a = lane; a < NK; a += 64) wk[a] = Rk[brow(a) * NRK + n];              // ku, kl
+            wave_lds_sync();
             for (int e = lane; e < n * n; e += 64) {
                 int i = e / n, j = e % n;
                 Ps[e] = 0.5 * (Pn[e] + Pn[j * n + i]);
             }
             if (lane < n) ps[lane] = pnew;
-            __syncthreads();
+            wave_lds_sync();
+            STAMP(15);
         }
         if (ok) { factor_ok = true; break; }
         if (zero && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
@@ -743,40 +864,65 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     st.reg_tier = tier;
     st.reg_last = reg;
 
+    wave_mem_sync();  // the Riccati slots stored above are read back by other lanes below
     // ---------------- forward sweep: du_k = Ku dx_k + ku, dyl_{k+1} = Kl dx_k + kl,
-    //                  dyc_k = P_{k+1} dx_{k+1} + p_{k+1}
+    //                  dyc_k = P_{k+1} dx_{k+1} + p_{k+1} + Jl_{k+1}^T dyl_{k+1}
+    // (the node-(k+1) line constraint was pushed back onto stage k, so V_{k+1} does not contain
+    // it but the q_{k+1} row of the KKT does).  Slot k+1 is prefetched while stage k runs.
+    double sr[NSR];
+#pragma unroll
+    for (int t = 0; t < NSR; t++) {
+        const int e = lane + 64 * t;
+        sr[t] = (e < SLOT) ? ((e < MB * NJ) ? G[e] : wv[e - MB * NJ]) : 0.0;  // slot 0
+    }
     for (int j = lane; j < n; j += 64) {
         dq[j] = 0.0; dqd[j] = 0.0;
-        xs[j] = q[j] + h * qd[j] - q[n + j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
+        xs[j] = cst[j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
     }
-    for (int a = lane; a < nf; a += 64) dF[a] = wv[NJ + a];
     for (int l = lane; l < nl; l += 64) { dyl[l] = 0.0; dyl[nl + l] = 0.0; }
-    __syncthreads();
-    for (int j = lane; j < n; j += 64) {  // dyc_0 = P_1 dx_1 + p_1 (slot 0)
-        double a = wv[NU + NL + j];
-        for (int i = 0; i < n; i++) a += G[(NU + NL) * n + j * n + i] * xs[i];
-        dyc[j] = a;
-    }
-    for (int k = 1; k < N; k++) {
-        const double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
+    for (int k = 0; k < N; k++) {
+        // slot k -> LDS; prefetch slot k+1
+#pragma unroll
+        for (int t = 0; t < NSR; t++) {
+            const int e = lane + 64 * t;
+            if (e < SLOT) Sl[e] = sr[t];
+        }
+        if (k + 1 < N) {
+            const double *Gn = G + (size_t)(k + 1) * MB * n, *wn = wv + (size_t)(k + 1) * MB;
+#pragma unroll
+            for (int t = 0; t < NSR; t++) {
+                const int e = lane + 64 * t;
+                sr[t] = (e < SLOT) ? ((e < MB * NJ) ? Gn[e] : wn[e - MB * NJ]) : 0.0;
+            }
+        }
+        wave_lds_sync();
+        const double *Gk = Sl, *wk = Sl + MB * NJ;
+        if (k == 0) {
+            for (int a = lane; a < nf; a += 64) dF[a] = wk[NJ + a];
+            for (int j = lane; j < n; j += 64) {  // dyc_0 = P_1 dx_1 + p_1 (stage-1 line is masked)
+                double a = wk[NU + NL + j];
+                for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * xs[i];
+                dyc[j] = a;
+            }
+            wave_lds_sync();
+            continue;
+        }
         for (int a = lane; a < NK; a += 64) {
             double v = wk[a];
             for (int i = 0; i < n; i++) v += Gk[a * n + i] * xs[i];
             us[a] = v;
         }
         for (int j = lane; j < n; j += 64) dq[k * n + j] = xs[j];
-        __syncthreads();
+        wave_lds_sync();
         for (int j = lane; j < n; j += 64) {
             dqd[k * n + j] = us[j];
-            cs[j] = xs[j] + h * us[j] + (q[k * n + j] + h * qd[k * n + j] - q[(k + 1) * n + j]);
+            cs[j] = xs[j] + h * us[j] + cst[k * n + j];
         }
         for (int a = lane; a < nf; a += 64) dF[k * NFA + a] = us[NJ + a];
-        if (k + 1 < N)
-            for (int l = lane; l < nl; l += 64) dyl[(k + 1) * nl + l] = ((nl > 0) && LINE_ON(k + 1)) ? us[NU + l] : 0.0;
-        __syncthreads();
-        // dyc_k = grad V_{k+1}(dx_{k+1}) + Jl_{k+1}^T dyl_{k+1}: the node-(k+1) line constraint was
-        // pushed back onto stage k, so V_{k+1} does not contain it but the q_{k+1} row of the KKT does
         const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
+        if (k + 1 < N)
+            for (int l = lane; l < nl; l += 64) dyl[(k + 1) * nl + l] = con1 ? us[NU + l] : 0.0;
+        wave_lds_sync();
         for (int j = lane; j < n; j += 64) {
             double a = wk[NU + NL + j];
             for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * cs[i];
@@ -785,7 +931,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
             dyc[k * n + j] = a;
             xs[j] = cs[j];
         }
-        __syncthreads();
+        wave_lds_sync();
     }
     for (int j = lane; j < n; j += 64) dq[N * n + j] = xs[j];
     __threadfence_block();
@@ -1001,6 +1147,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     }
     STAMP(6);
     STAMP_COUNT(10, 1);
+    STAMP_FLUSH;
     if (lane == 0) {
         st.iter++;
         st.mu = mu;
@@ -1058,8 +1205,18 @@ struct IpmLaunch {
         if (phase == 0)
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3((unsigned)((nodes + NPB - 1) / NPB)), dim3(256), 0, s,
                                M, F, C, A, batch);
-        else
-            hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+        else {
+            const size_t dyn = ipm_dyn_lds(C.N);
+            if (dyn > 64 * 1024)
+                (void)hipFuncSetAttribute((const void *)k_ipm_iter<NJ, NF, NL>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+            hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), dyn, s, M, F, C, A, batch);
+        }
+    }
+    // dynamic LDS of k_ipm_iter: per-stage g_k (NV), c_k (NJ), e_k (NL), y_tau + D r_tau (NJ), dD (NJ)
+    static size_t ipm_dyn_lds(int N) {
+        constexpr int NV = 2 * NJ + NF;
+        return (size_t)N * (NV + 3 * NJ + (NL > 0 ? NL : 1)) * sizeof(double);
     }
     static void output(const OcpConst &C, const IpmArrays &A, int batch, double *w, int *status, int *iters,
                        double *kkt, double *obj, hipStream_t s) {
@@ -1102,6 +1259,6 @@ extern "C" int mf_debug_trace(double *out, int nprob) {
 #ifdef MF_PHASE_STAMPS
 extern "C" int mf_debug_phase_stamps(unsigned long long *out, int nprob) {
     if (nprob > 4096) nprob = 4096;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mf::mf_stamp_buf), sizeof(unsigned long long) * 16 * nprob) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mf::mf_stamp_buf), sizeof(unsigned long long) * 32 * nprob) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -28,14 +28,21 @@ Q0 = PR.pilz6_batch_q0(B, seed=0)
 LR = np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in Q0])
 res = ocp.solve(Q0, line_ref=LR, tol=1e-8, constr_viol_tol=1e-8, max_iter=300, F_init=PR.BENCH_F_INIT)
 L = _lib.lib()
-buf = (C.c_ulonglong * (16 * B))()
+buf = (C.c_ulonglong * (32 * B))()
 L.mf_debug_phase_stamps(buf, B)
-a = np.array(buf, dtype=np.float64).reshape(B, 16)
-names = ["opt-err+mu", "barrier", "kkt-factor", "backsub+recover", "ftb+merit0+gdot", "linesearch", "update"]
-tot = a[:, :7].sum(1)
+a = np.array(buf, dtype=np.float64).reshape(B, 32)
+# KKT sub-phases (per stage, summed): 7 H to LDS, 11 s=Pc+p + slot stores, 12 block assembly,
+# 13 Bunch-Kaufman factor, 14 solve, 15 P update; slot 2 keeps the rest of the KKT phase
+cols = [0, 1, 2, 7, 11, 12, 13, 14, 15, 3, 4, 5, 6]
+names = ["opt-err+mu", "barrier", "kkt-other", " kkt:H->LDS", " kkt:s+slot", " kkt:assemble", " kkt:BK-factor",
+         " kkt:BK-solve", " kkt:P-update", "backsub+recover", "ftb+merit0+gdot", "linesearch", "update"]
+a_ = a
+a = a_[:, cols]
+tot = a.sum(1)
 print("status", np.bincount(res.status), "mean iters", res.iters.mean())
-it = a[:, 10]
+it = a_[:, 10]
 print("per-iteration cycles (median over problems):", np.median(tot / it))
 for i, nm in enumerate(names):
     print(f"{nm:18s} {np.median(a[:, i] / it):12.0f} cyc/iter  {100 * a[:, i].sum() / tot.sum():5.1f}%")
-print("inertia tries / iter", np.mean(a[:, 8] / it), " line-search trials / iter", np.mean(a[:, 9] / it))
+print("inertia tries / iter", np.mean(a_[:, 8] / it), " line-search trials / iter", np.mean(a_[:, 9] / it))
+print("stage factorisations / iter", np.mean(a_[:, 17] / it), " pivoted fallbacks / iter", np.mean(a_[:, 16] / it))
