@@ -418,7 +418,7 @@ static int ensure_ws(mf_problem *p, int batch) {
         {&A.dzqL, S.q}, {&A.dzqU, S.q}, {&A.dzdL, S.u}, {&A.dzdU, S.u}, {&A.dvL, S.u}, {&A.dvU, S.u},
         {&A.tau, S.u}, {&A.Jt, S.jt}, {&A.line, S.l}, {&A.Jl, S.jl}, {&A.W, S.w}, {&A.gf, S.gf}, {&A.cost, S.cost},
         {&A.Sxq, S.q}, {&A.gphq, S.q}, {&A.Sxd, S.u}, {&A.gphd, S.u}, {&A.Ss, S.u}, {&A.gphs, S.u},
-        {&A.G, S.G}, {&A.wv, S.wv}, {&A.q0, (size_t)C.n}, {&A.lref, 2},
+        {&A.G, S.G}, {&A.wv, S.wv}, {&A.stg, S.stg}, {&A.q0, (size_t)C.n}, {&A.lref, 2},
     };
     for (auto &it : items) {
         double *ptr = nullptr;

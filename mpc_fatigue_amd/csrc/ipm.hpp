@@ -42,6 +42,8 @@ struct IpmArrays {
     double *Sxq, *gphq, *Sxd, *gphd, *Ss, *gphs;
     // block LDL^T recursion
     double *G, *wv;
+    // per-stage Riccati inputs [N x (g_k | c_k | e_k | dD_k)] then y_tau + D_tau r_tau (N x n)
+    double *stg;
     // per-problem data
     double *q0, *lref;
     const double *tau_lo, *tau_hi;  // shared N x n
@@ -51,7 +53,7 @@ struct IpmArrays {
 
 // sizes (doubles) per problem
 struct IpmSizes {
-    size_t q, u, f, l, jt, jl, w, gf, cost, G, wv;
+    size_t q, u, f, l, jt, jl, w, gf, cost, G, wv, stg;
 };
 
 __host__ __device__ inline IpmSizes ipm_sizes(const OcpConst &c) {
@@ -67,6 +69,7 @@ __host__ __device__ inline IpmSizes ipm_sizes(const OcpConst &c) {
     s.cost = (size_t)c.N;
     s.G = (size_t)c.N * c.mb * c.n;
     s.wv = (size_t)(c.N + 1) * c.mb;
+    s.stg = (size_t)c.N * (c.nv + 3 * c.n + (c.nl > 0 ? c.nl : 1));
     return s;
 }
 

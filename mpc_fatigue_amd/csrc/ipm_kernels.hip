@@ -17,6 +17,7 @@
 #include "bk_wave.hpp"
 #include "dyn.hpp"
 #include "ipm.hpp"
+#include "stage_ns.hpp"
 
 namespace mf {
 
@@ -97,6 +98,19 @@ template <class T> __device__ __forceinline__ void stage_lds(T *dst, const T *sr
     for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
 }
 
+// LDS image of a DevModel holding only its first NJ joints (the kernels of an NJ-joint
+// instantiation never index past joint NJ-1): 0.4 KB per joint instead of the full
+// MF_MAX_JOINTS table, which keeps more workgroups resident per CU.
+template <int NJ> struct ModelLds {
+    static constexpr int WORDS = (int)((offsetof(DevModel, j) + NJ * sizeof(DevJoint) + sizeof(double) - 1) / sizeof(double));
+    double w[WORDS];
+    __device__ __forceinline__ void load(const DevModel *g) {
+        const double *s = reinterpret_cast<const double *>(g);
+        for (int i = threadIdx.x; i < WORDS; i += blockDim.x) w[i] = s[i];
+    }
+    __device__ __forceinline__ const DevModel &get() const { return *reinterpret_cast<const DevModel *>(w); }
+};
+
 // ============================================================== eval: node derivatives
 // Lanes (problem, node, direction v), NV = 2 n + n_f lanes per node, NPB nodes per
 // block.  Each lane runs node_fwd_rev<Dual> (adj.hpp) with tangent e_v and gets tau,
@@ -141,10 +155,11 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     constexpr int NV = 2 * NJ + NF;
     constexpr int NFA = NF > 0 ? NF : 1;
     constexpr int NPB = 256 / NV;
-    __shared__ DevModel M;
+    __shared__ ModelLds<NJ> Ml;
+    const DevModel &M = Ml.get();
     __shared__ DevFrame F;
     __shared__ double Js[NPB][NJ][NV], Hs[NPB][NV][NV], Ts[NPB][NJ], Cs[NPB][NJ];
-    stage_lds(&M, Mg);
+    Ml.load(Mg);
     stage_lds(&F, Fg);
     const int tid = threadIdx.x, g = tid / NV, v = tid % NV;
     const int N = C.N;
@@ -284,9 +299,10 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
 template <int NJ, int NF, int NL>
 __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
-    __shared__ DevModel M;
+    __shared__ ModelLds<NJ> Ml;
+    const DevModel &M = Ml.get();
     __shared__ DevFrame F;
-    stage_lds(&M, Mg);
+    Ml.load(Mg);
     stage_lds(&F, Fg);
     __syncthreads();
     const int b = blockIdx.x, lane = threadIdx.x;
@@ -380,16 +396,23 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     constexpr int NFA = NF > 0 ? NF : 1;
     constexpr int NLA = NL > 0 ? NL : 1;
     constexpr int MB = 3 * NJ + NF + NL;
-    __shared__ DevModel M;
+    __shared__ ModelLds<NJ> Ml;
+    const DevModel &M = Ml.get();
     __shared__ DevFrame F;
-    __shared__ double Dd_s[NJ], Ss_s[NJ], rdd_s[NJ];
     __shared__ int perm[MB], piv[MB];
     const int b = blockIdx.x, lane = threadIdx.x;
     if (b >= batch) return;
     ProbState st = A.st[b];
     if (st.status != ST_RUNNING) return;
-    stage_lds(&M, Mg);
+    Ml.load(Mg);
     stage_lds(&F, Fg);
+    __shared__ double Bnd[4 * NJ];  // q_lo, q_hi, qd_lo, qd_hi (kernel-argument arrays read per element)
+    if (lane < NJ) {
+        Bnd[lane] = C.q_lo[lane];
+        Bnd[NJ + lane] = C.q_hi[lane];
+        Bnd[2 * NJ + lane] = C.qd_lo[lane];
+        Bnd[3 * NJ + lane] = C.qd_hi[lane];
+    }
     __syncthreads();
     STAMP_INIT;
 
@@ -411,7 +434,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     double *G = A.G + b * S.G, *wv = A.wv + b * S.wv;
     const double *lref = A.lref + b * 2;
     const double *tlo = A.tau_lo, *thi = A.tau_hi;
-    const double *QLO = C.q_lo, *QHI = C.q_hi, *DLO = C.qd_lo, *DHI = C.qd_hi;
+    const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
 #define TACT(k, j) (hasb(tlo[(k) * n + (j)]) || hasb(thi[(k) * n + (j)]))
 
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
@@ -419,56 +442,115 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     double mu = st.mu, nu = st.nu;
 
     // ---------------- optimality error
+    // Element loops of one problem run in chunks of UB elements per lane.  A chunk issues every
+    // load first (indices clamped into range, results past the end discarded) and only then
+    // computes and stores, so it costs one global-memory round trip instead of one per element:
+    // one wave per problem has no other waves of its own to hide that latency behind.
+    constexpr int UB = 4;
     double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sum_mult = 0, sum_bmult = 0;
     int n_mult = 0, n_bmult = 0;
-    for (int e = lane; e < N * n; e += 64) {  // q rows, k = 1..N
-        int k = e / n + 1, j = e % n, i = k * n + j;
-        double r;
-        if (k < N) {
-            r = gf[k * NV + j] + yc[k * n + j] - yc[(k - 1) * n + j];
-            for (int l = 0; l < nl; l++) r += Jl[(k * nl + l) * n + j] * yl[k * nl + l];
-            for (int jj = 0; jj < n; jj++) r += Jt[((size_t)k * n + jj) * NV + j] * yd[k * n + jj];
-        } else {
-            r = -yc[(N - 1) * n + j];
+    auto comp = [&](double z, double gap) {
+        const double c = z * gap;
+        cinf0 = fmax(cinf0, fabs(c));
+        cinfm = fmax(cinfm, fabs(c - mu));
+        sum_bmult += z;
+        n_bmult++;
+    };
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {  // q rows, k = 1..N
+        double r[UB], x[UB], zl[UB], zu[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            const int k = e / n + 1, j = e % n, i = k * n + j, kk = min(k, N - 1);
+            double a = gf[kk * NV + j] + yc[kk * n + j] - yc[(k - 1) * n + j];
+#pragma unroll
+            for (int l = 0; l < NL; l++) a += Jl[(kk * nl + l) * n + j] * yl[kk * nl + l];
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) a += Jt[((size_t)kk * n + jj) * NV + j] * yd[kk * n + jj];
+            const double ycl = yc[(N - 1) * n + j];
+            zl[u] = zqL[i];
+            zu[u] = zqU[i];
+            x[u] = q[i];
+            r[u] = (k < N ? a : -ycl) - zl[u] + zu[u];
         }
-        r += -zqL[i] + zqU[i];
-        dinf = fmax(dinf, fabs(r));
-        double x = q[i];
-        if (hasb(QLO[j])) { double c = zqL[i] * (x - QLO[j]); cinf0 = fmax(cinf0, fabs(c)); cinfm = fmax(cinfm, fabs(c - mu)); sum_bmult += zqL[i]; n_bmult++; }
-        if (hasb(QHI[j])) { double c = zqU[i] * (QHI[j] - x); cinf0 = fmax(cinf0, fabs(c)); cinfm = fmax(cinfm, fabs(c - mu)); sum_bmult += zqU[i]; n_bmult++; }
-    }
-    for (int e = lane; e < N * n; e += 64) {
-        int k = e / n, j = e % n, i = e;
-        if (k > 0) {
-            double r = gf[k * NV + n + j] + h * yc[i];
-            for (int jj = 0; jj < n; jj++) r += Jt[((size_t)k * n + jj) * NV + n + j] * yd[k * n + jj];
-            r += -zdL[i] + zdU[i];
-            dinf = fmax(dinf, fabs(r));
-            double x = qd[i];
-            if (hasb(DLO[j])) { double c = zdL[i] * (x - DLO[j]); cinf0 = fmax(cinf0, fabs(c)); cinfm = fmax(cinfm, fabs(c - mu)); sum_bmult += zdL[i]; n_bmult++; }
-            if (hasb(DHI[j])) { double c = zdU[i] * (DHI[j] - x); cinf0 = fmax(cinf0, fabs(c)); cinfm = fmax(cinfm, fabs(c - mu)); sum_bmult += zdU[i]; n_bmult++; }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * n) {
+                const int j = e % n;
+                dinf = fmax(dinf, fabs(r[u]));
+                if (hasb(QLO[j])) comp(zl[u], x[u] - QLO[j]);
+                if (hasb(QHI[j])) comp(zu[u], QHI[j] - x[u]);
+            }
         }
-        if (TACT(k, j)) {
-            double r = -yd[i] - vL[i] + vU[i];
-            dinf = fmax(dinf, fabs(r));
-            double x = s[i];
-            if (hasb(tlo[i])) { double c = vL[i] * (x - tlo[i]); cinf0 = fmax(cinf0, fabs(c)); cinfm = fmax(cinfm, fabs(c - mu)); sum_bmult += vL[i]; n_bmult++; }
-            if (hasb(thi[i])) { double c = vU[i] * (thi[i] - x); cinf0 = fmax(cinf0, fabs(c)); cinfm = fmax(cinfm, fabs(c - mu)); sum_bmult += vU[i]; n_bmult++; }
-            pinf = fmax(pinf, fabs(tau[i] - s[i]));
-            sum_mult += fabs(yd[i]); n_mult++;
+    }
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {  // qd rows (k >= 1), torque rows, continuity
+        double r[UB], x[UB], zl[UB], zu[UB], r2[UB], xs[UB], vl[UB], vu[UB], lo[UB], hi[UB], pt[UB], pc[UB], ydv[UB], ycv[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            const int k = e / n, j = e % n;
+            double a = gf[k * NV + n + j] + h * yc[e];
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) a += Jt[((size_t)k * n + jj) * NV + n + j] * yd[k * n + jj];
+            zl[u] = zdL[e]; zu[u] = zdU[e]; x[u] = qd[e];
+            r[u] = a - zl[u] + zu[u];
+            vl[u] = vL[e]; vu[u] = vU[e]; xs[u] = s[e]; lo[u] = tlo[e]; hi[u] = thi[e];
+            ydv[u] = yd[e]; ycv[u] = yc[e];
+            r2[u] = -ydv[u] - vl[u] + vu[u];
+            pt[u] = fabs(tau[e] - xs[u]);
+            pc[u] = fabs(q[k * n + j] + h * x[u] - q[(k + 1) * n + j]);
         }
-        pinf = fmax(pinf, fabs(q[k * n + j] + h * qd[i] - q[(k + 1) * n + j]));
-        sum_mult += fabs(yc[i]); n_mult++;
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * n) {
+                const int k = e / n, j = e % n;
+                if (k > 0) {
+                    dinf = fmax(dinf, fabs(r[u]));
+                    if (hasb(DLO[j])) comp(zl[u], x[u] - DLO[j]);
+                    if (hasb(DHI[j])) comp(zu[u], DHI[j] - x[u]);
+                }
+                if (hasb(lo[u]) || hasb(hi[u])) {
+                    dinf = fmax(dinf, fabs(r2[u]));
+                    if (hasb(lo[u])) comp(vl[u], xs[u] - lo[u]);
+                    if (hasb(hi[u])) comp(vu[u], hi[u] - xs[u]);
+                    pinf = fmax(pinf, pt[u]);
+                    sum_mult += fabs(ydv[u]); n_mult++;
+                }
+                pinf = fmax(pinf, pc[u]);
+                sum_mult += fabs(ycv[u]); n_mult++;
+            }
+        }
     }
-    for (int e = lane; e < N * nf; e += 64) {
-        int k = e / nf, a = e % nf;
-        double r = gf[k * NV + 2 * n + a];
-        for (int jj = 0; jj < n; jj++) r += Jt[((size_t)k * n + jj) * NV + 2 * n + a] * yd[k * n + jj];
-        dinf = fmax(dinf, fabs(r));
+    for (int e0 = lane; e0 < N * nf; e0 += 64 * UB) {  // force rows
+        double r[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * nf - 1);
+            const int k = e / nf, a = e % nf;
+            double v = gf[k * NV + 2 * n + a];
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) v += Jt[((size_t)k * n + jj) * NV + 2 * n + a] * yd[k * n + jj];
+            r[u] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++)
+            if (e0 + 64 * u < N * nf) dinf = fmax(dinf, fabs(r[u]));
     }
-    for (int e = lane; e < N * nl; e += 64) {
-        int k = e / nl;
-        if (LINE_ON(k)) { pinf = fmax(pinf, fabs(line[e])); sum_mult += fabs(yl[e]); n_mult++; }
+    for (int e0 = lane; e0 < N * nl; e0 += 64 * UB) {  // line rows
+        double lv[UB], yv[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * nl - 1);
+            lv[u] = line[e];
+            yv[u] = yl[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * nl && LINE_ON(e / nl)) { pinf = fmax(pinf, fabs(lv[u])); sum_mult += fabs(yv[u]); n_mult++; }
+        }
     }
     dinf = wave_max(dinf); pinf = wave_max(pinf); cinf0 = wave_max(cinf0); cinfm = wave_max(cinfm);
     sum_mult = wave_sum(sum_mult); sum_bmult = wave_sum(sum_bmult);
@@ -509,22 +591,26 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         if (mnew >= mu) break;
         mu = mnew;
         double cm = 0.0;
-        for (int e = lane; e < N * n; e += 64) {
-            int k = e / n + 1, j = e % n, i = k * n + j;
-            double x = q[i];
-            if (hasb(QLO[j])) cm = fmax(cm, fabs(zqL[i] * (x - QLO[j]) - mu));
-            if (hasb(QHI[j])) cm = fmax(cm, fabs(zqU[i] * (QHI[j] - x) - mu));
-        }
-        for (int e = lane; e < N * n; e += 64) {
-            int k = e / n, j = e % n, i = e;
-            if (k > 0) {
-                double x = qd[i];
-                if (hasb(DLO[j])) cm = fmax(cm, fabs(zdL[i] * (x - DLO[j]) - mu));
-                if (hasb(DHI[j])) cm = fmax(cm, fabs(zdU[i] * (DHI[j] - x) - mu));
+        for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+            double cp[6][UB];
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = min(e0 + 64 * u, N * n - 1);
+                const int i = e + n, j = e % n;
+                const double xq = q[i], xd = qd[e], xs = s[e], l = tlo[e], hh = thi[e];
+                const bool in = e0 + 64 * u < N * n, kq = e / n > 0;
+                cp[0][u] = (in && hasb(QLO[j])) ? zqL[i] * (xq - QLO[j]) : NAN;
+                cp[1][u] = (in && hasb(QHI[j])) ? zqU[i] * (QHI[j] - xq) : NAN;
+                cp[2][u] = (in && kq && hasb(DLO[j])) ? zdL[e] * (xd - DLO[j]) : NAN;
+                cp[3][u] = (in && kq && hasb(DHI[j])) ? zdU[e] * (DHI[j] - xd) : NAN;
+                cp[4][u] = (in && hasb(l)) ? vL[e] * (xs - l) : NAN;
+                cp[5][u] = (in && hasb(hh)) ? vU[e] * (hh - xs) : NAN;
             }
-            double x = s[i];
-            if (hasb(tlo[i])) cm = fmax(cm, fabs(vL[i] * (x - tlo[i]) - mu));
-            if (hasb(thi[i])) cm = fmax(cm, fabs(vU[i] * (thi[i] - x) - mu));
+#pragma unroll
+            for (int u = 0; u < UB; u++)
+#pragma unroll
+                for (int p = 0; p < 6; p++)
+                    if (!isnan(cp[p][u])) cm = fmax(cm, fabs(cp[p][u] - mu));
         }
         cinfm = wave_max(cm);
         Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
@@ -534,31 +620,53 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     STAMP(0);
 
     // ---------------- barrier Sigma and gradients
-    for (int e = lane; e < (N + 1) * n; e += 64) {
-        int k = e / n, j = e % n;
-        double sx = 0, gp = 0;
-        if (k > 0) {
-            double x = q[e];
-            sx = sigma_pair(zqL[e], zqU[e], x, QLO[j], QHI[j]);
-            if (hasb(QLO[j])) gp -= mu / (x - QLO[j]);
-            if (hasb(QHI[j])) gp += mu / (QHI[j] - x);
+    for (int e0 = lane; e0 < (N + 1) * n; e0 += 64 * UB) {
+        double x[UB], zl[UB], zu[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, (N + 1) * n - 1);
+            x[u] = q[e]; zl[u] = zqL[e]; zu[u] = zqU[e];
         }
-        Sxq[e] = sx; gphq[e] = gp;
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < (N + 1) * n) {
+                const int k = e / n, j = e % n;
+                double sx = 0, gp = 0;
+                if (k > 0) {
+                    sx = sigma_pair(zl[u], zu[u], x[u], QLO[j], QHI[j]);
+                    if (hasb(QLO[j])) gp -= mu / (x[u] - QLO[j]);
+                    if (hasb(QHI[j])) gp += mu / (QHI[j] - x[u]);
+                }
+                Sxq[e] = sx; gphq[e] = gp;
+            }
+        }
     }
-    for (int e = lane; e < N * n; e += 64) {
-        int k = e / n, j = e % n;
-        double sx = 0, gp = 0, ss = 0, gs = 0;
-        if (k > 0) {
-            double x = qd[e];
-            sx = sigma_pair(zdL[e], zdU[e], x, DLO[j], DHI[j]);
-            if (hasb(DLO[j])) gp -= mu / (x - DLO[j]);
-            if (hasb(DHI[j])) gp += mu / (DHI[j] - x);
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        double x[UB], zl[UB], zu[UB], xs[UB], vl[UB], vu[UB], lo[UB], hi[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            x[u] = qd[e]; zl[u] = zdL[e]; zu[u] = zdU[e];
+            xs[u] = s[e]; vl[u] = vL[e]; vu[u] = vU[e]; lo[u] = tlo[e]; hi[u] = thi[e];
         }
-        double x = s[e];
-        ss = sigma_pair(vL[e], vU[e], x, tlo[e], thi[e]);
-        if (hasb(tlo[e])) gs -= mu / (x - tlo[e]);
-        if (hasb(thi[e])) gs += mu / (thi[e] - x);
-        Sxd[e] = sx; gphd[e] = gp; Ss[e] = ss; gphs[e] = gs;
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * n) {
+                const int k = e / n, j = e % n;
+                double sx = 0, gp = 0, gs = 0;
+                if (k > 0) {
+                    sx = sigma_pair(zl[u], zu[u], x[u], DLO[j], DHI[j]);
+                    if (hasb(DLO[j])) gp -= mu / (x[u] - DLO[j]);
+                    if (hasb(DHI[j])) gp += mu / (DHI[j] - x[u]);
+                }
+                const double ss = sigma_pair(vl[u], vu[u], xs[u], lo[u], hi[u]);
+                if (hasb(lo[u])) gs -= mu / (xs[u] - lo[u]);
+                if (hasb(hi[u])) gs += mu / (hi[u] - xs[u]);
+                Sxd[e] = sx; gphd[e] = gp; Ss[e] = ss; gphs[e] = gs;
+            }
+        }
     }
     __threadfence_block();
     __syncthreads();
@@ -588,59 +696,87 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     constexpr int NSR = (SLOT + 63) / 64;
     __shared__ double Hs[NVV];
     __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], Pn[NJ * NJ];
-    __shared__ double Ks[NK * LDK], Rk[NK * NRK], Yk[NK * NRK];
+    __shared__ double Ks[NK * LDK], Rk[NK * NRK];
     __shared__ double Gl[NLA2 * NJ];
+    __shared__ double Ss5[(NU > 2 ? NU - 2 : 1) * (NU > 2 ? NU - 2 : 1)];  // reduced Hessian (stage_ns.hpp)
     __shared__ double xs[NJ], us[NU + NLA2], cs[NJ];
     __shared__ double Sl[SLOT];
     __shared__ double Jl_s[NJ * NV];  // J_k (torque Jacobian) of the stage, regularised tries only
-    extern __shared__ double dyn_lds[];
-    double *gst = dyn_lds;                    // N x NV   stage gradients g_k
-    double *cst = gst + (size_t)N * NV;       // N x NJ   c_k = q_k + h qd_k - q_{k+1}
-    double *est = cst + (size_t)N * NJ;       // N x NLA2 e_k = line_{k+1} + Jl_{k+1} c_k
-    double *wst = est + (size_t)N * NLA2;     // N x NJ   y_tau + D_tau r_tau (torque rows)
-    double *dst = wst + (size_t)N * NJ;       // N x NJ   D_tau(dw, dc) - Sigma_s (0 unless dw, dc != 0)
-    // g_k for all stages at the current (dw, dc): exactly the primal rows of the KKT right-hand side
+    // per-stage inputs of the recursion, computed for all stages at once by the whole wave (global
+    // scratch, stage k contiguous): g_k (NV), c_k = q_k + h qd_k - q_{k+1} (NJ),
+    // e_k = line_{k+1} + Jl_{k+1} c_k (NLA2), dD_k = D_tau(dw, dc) - Sigma_s (NJ); then
+    // y_tau + D_tau r_tau (N x NJ, used inside prep only)
+    constexpr int SG = NV + 2 * NJ + NLA2;
+    double *stg = A.stg + b * S.stg;
+    double *wst = stg + (size_t)N * SG;
+    __shared__ double Stg[SG];  // stage k's block, staged from a register prefetch
     auto prep_stages = [&](double dwv, double dcv) {
-        for (int e = lane; e < N * n; e += 64) {
-            const int k = e / n, j = e % n;
-            double wv_ = yd[e], dD = 0.0;
-            if (TACT(k, j)) {
-                const double sg = Ss[e] + dwv;
-                const double Dd = sg / (1.0 + dcv * sg);
-                wv_ += Dd * ((tau[e] - s[e]) + (gphs[e] - yd[e]) / sg);
-                dD = Dd - Ss[e];
-            }
-            wst[e] = wv_;
-            dst[e] = dD;
-            cst[e] = q[e] + h * qd[e] - q[e + n];
-        }
-        wave_lds_sync();
-        for (int e = lane; e < N * NV; e += 64) {
-            const int k = e / NV, u = e % NV;
-            double g = gf[e];
-            const double *Jtk = Jt + (size_t)k * n * NV;
+        for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+            double ydv[UB], ssv[UB], tv[UB], sv[UB], gv[UB], lo[UB], hi[UB], qa[UB], qdv[UB], qb[UB];
 #pragma unroll
-            for (int jj = 0; jj < NJ; jj++) g += Jtk[jj * NV + u] * wst[k * n + jj];
-            if (u < n) {
-                g += gphq[k * n + u] + yc[k * n + u] - (k > 0 ? yc[(k - 1) * n + u] : 0.0);
-#pragma unroll
-                for (int l = 0; l < NL; l++) g += Jl[(k * nl + l) * n + u] * yl[k * nl + l];
-            } else if (u < 2 * n) {
-                g += gphd[k * n + u - n] + h * yc[k * n + u - n];
+            for (int u = 0; u < UB; u++) {
+                const int e = min(e0 + 64 * u, N * n - 1);
+                ydv[u] = yd[e]; ssv[u] = Ss[e]; tv[u] = tau[e]; sv[u] = s[e]; gv[u] = gphs[e];
+                lo[u] = tlo[e]; hi[u] = thi[e]; qa[u] = q[e]; qdv[u] = qd[e]; qb[u] = q[e + n];
             }
-            gst[e] = g;
-        }
-        for (int e = lane; e < N * nl; e += 64) {
-            const int k = e / nl, l = e % nl;
-            double a = 0.0;
-            if (LINE_ON(k + 1) && k + 1 <= N - 1) {
-                a = line[(k + 1) * nl + l];
 #pragma unroll
-                for (int i = 0; i < NJ; i++) a += Jl[((size_t)(k + 1) * nl + l) * n + i] * cst[k * n + i];
+            for (int u = 0; u < UB; u++) {
+                const int e = e0 + 64 * u;
+                if (e < N * n) {
+                    double wv_ = ydv[u], dD = 0.0;
+                    if (hasb(lo[u]) || hasb(hi[u])) {
+                        const double sg = ssv[u] + dwv;
+                        const double Dd = sg / (1.0 + dcv * sg);
+                        wv_ += Dd * ((tv[u] - sv[u]) + (gv[u] - ydv[u]) / sg);
+                        dD = Dd - ssv[u];
+                    }
+                    const int k = e / n, j = e % n;
+                    wst[e] = wv_;
+                    stg[k * SG + NV + NJ + NLA2 + j] = dD;
+                    stg[k * SG + NV + j] = qa[u] + h * qdv[u] - qb[u];
+                }
             }
-            est[k * NLA2 + l] = a;
         }
-        wave_lds_sync();
+        wave_mem_sync();  // wst / c_k are read back by other lanes
+        for (int e0 = lane; e0 < N * NV; e0 += 64 * UB) {
+            double g[UB];
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = min(e0 + 64 * u, N * NV - 1);
+                const int k = e / NV, v = e % NV;
+                const int vq = v < n ? v : 0, vd = (v >= n && v < 2 * n) ? v - n : 0;
+                double a = gf[e];
+                const double *Jtk = Jt + (size_t)k * n * NV;
+#pragma unroll
+                for (int jj = 0; jj < NJ; jj++) a += Jtk[jj * NV + v] * wst[k * n + jj];
+                double aq = gphq[k * n + vq] + yc[k * n + vq] - (k > 0 ? yc[(k > 0 ? k - 1 : 0) * n + vq] : 0.0);
+#pragma unroll
+                for (int l = 0; l < NL; l++) aq += Jl[(k * nl + l) * n + vq] * yl[k * nl + l];
+                const double ad = gphd[k * n + vd] + h * yc[k * n + vd];
+                g[u] = a + (v < n ? aq : (v < 2 * n ? ad : 0.0));
+            }
+#pragma unroll
+            for (int u = 0; u < UB; u++)
+                if (e0 + 64 * u < N * NV) stg[((e0 + 64 * u) / NV) * SG + (e0 + 64 * u) % NV] = g[u];
+        }
+        for (int e0 = lane; e0 < N * nl; e0 += 64 * UB) {
+            double a[UB];
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = min(e0 + 64 * u, N * nl - 1);
+                const int k = e / nl, l = e % nl, k1 = min(k + 1, N - 1);
+                double v = line[k1 * nl + l];
+#pragma unroll
+                for (int i = 0; i < NJ; i++) v += Jl[((size_t)k1 * nl + l) * n + i] * stg[k * SG + NV + i];
+                a[u] = (LINE_ON(k + 1) && k + 1 <= N - 1) ? v : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = e0 + 64 * u;
+                if (e < N * nl) stg[(e / nl) * SG + NV + NJ + e % nl] = a[u];
+            }
+        }
+        wave_mem_sync();  // the stage loop reads the blocks back
     };
     double dw = 0.0, dc = 0.0, dFr = 0.0;
     const int reg_tier0 = st.reg_tier;
@@ -681,9 +817,11 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
             jr[t] = (dreg && e < NJV) ? Jt[(size_t)(N - 1) * NJV + e] : 0.0;
         }
         double glr = 0.0;  // Jl_{k+1} entry of this lane for the next stage
+        double sgr = (lane < SG) ? stg[(size_t)(N - 1) * SG + lane] : 0.0;  // stage block, one ahead
         wave_lds_sync();
         for (int k = N - 1; k >= 0; k--) {
             // ---- H_k = H0_k (+ regularisation) into LDS; prefetch H0_{k-1}, Jl_k (, J_{k-1})
+            if (lane < SG) Stg[lane] = sgr;
             if (dreg) {
 #pragma unroll
                 for (int t = 0; t < NJR; t++) {
@@ -692,7 +830,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
                 }
                 wave_lds_sync();
             }
-            const double *dDk = dst + (size_t)k * n;
+            const double *dDk = Stg + NV + NJ + NLA2;
 #pragma unroll
             for (int t = 0; t < NHR; t++) {
                 const int e = lane + 64 * t;
@@ -715,6 +853,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
                     hr[t] = (e < NVV) ? W[(size_t)(k - 1) * NVV + e] : 0.0;
                 }
                 glr = (lane < nl * n) ? Jl[(size_t)k * nl * n + lane] : 0.0;
+                sgr = (lane < SG) ? stg[(size_t)(k - 1) * SG + lane] : 0.0;
                 if (dreg)
 #pragma unroll
                     for (int t = 0; t < NJR; t++) {
@@ -724,7 +863,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
             }
             // s = P c + p ; keep P_{k+1}, p_{k+1} for the forward sweep
             double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
-            const double *ck = cst + (size_t)k * n;
+            const double *ck = Stg + NV;
             if (lane < n) {
                 const int j = lane;
                 double a = ps[j];
@@ -736,7 +875,7 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
             for (int e = lane; e < n * n; e += 64) Gk[(NU + NL) * n + e] = Ps[e];
             wave_lds_sync();
             STAMP(11);
-            const double *gsk = gst + (size_t)k * NV;
+            const double *gsk = Stg;
             if (k == 0) {
                 // only dF_0 is free (q_0, qd_0 fixed; the stage-1 line constraint is masked)
                 if (nf > 0) {
@@ -753,55 +892,65 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
                 break;
             }
             const bool con = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
-            const double *elk = est + (size_t)k * NLA2;
-            // ---- stage block [[Quu, Du^T], [Du, -dc]] and right-hand sides -[Qux | qu ; G | e]
-            // Block rows order the controls as (F, qd): with active torque bounds the force
-            // carries the large curvature Sigma_s (J^T F)^2 and the joint velocities couple to it
-            // weakly, so natural-order 1x1 pivots pass the Bunch-Kaufman test (ldl_schur_regs).
-            // uo(a): control index (qd 0..n-1, F n..) of block row a < NU.
+            const double *elk = Stg + NV + NJ;
+            // ---- stage solve: null-space elimination (stage_ns.hpp) when the two line rows are
+            // active and dc = 0, the pivoted Bunch-Kaufman block otherwise
             auto uo = [&](int a) { return a < NF ? NJ + a : a - NF; };
-            for (int e = lane; e < NK * NK; e += 64) {
-                int a = e / NK, c = e % NK;
-                double val;
-                if (a < NU && c < NU) {
-                    const int ua = uo(a), uc = uo(c);
-                    val = Hs[(n + ua) * NV + n + uc];
-                    if (ua < n && uc < n) val += h * h * Ps[ua * n + uc];
-                } else if (a >= NU && c >= NU) {
-                    val = (a == c) ? (con ? -dc : -1.0) : 0.0;
-                } else {
-                    int l = (a >= NU) ? a - NU : c - NU, v = uo((a >= NU) ? c : a);
-                    val = (con && v < n) ? h * Gl[l * n + v] : 0.0;
-                }
-                Ks[a * LDK + c] = val;
+            int nsr = -1;
+            if constexpr (NL == 2) {
+                if (con && dc == 0.0) nsr = stage_nullspace<NJ, NF, NV, NRK>(Hs, Ps, ss, Gl, gsk, elk, h, Ss5, Rk);
             }
-            for (int e = lane; e < NK * NRK; e += 64) {
-                int a = e / NRK, c = e % NRK;
-                double val;
-                if (a < NU) {
-                    const int ua = uo(a);
-                    if (c < n) val = -(Hs[(n + ua) * NV + c] + (ua < n ? h * Ps[ua * n + c] : 0.0));
-                    else val = -(gsk[n + ua] + (ua < n ? h * ss[ua] : 0.0));
-                } else {
-                    int l = a - NU;
-                    val = con ? -(c < n ? Gl[l * n + c] : elk[l]) : 0.0;
-                }
-                Rk[e] = val;
-            }
-            wave_lds_sync();
-            STAMP(12);
-            BKInertia in;
-            const bool fast = ldl_schur_regs<LDK, NRK, NU, NL>(Ks, Rk, NRK, in);
             STAMP(13);
-            STAMP_COUNT(16, fast ? 0 : 1);
             STAMP_COUNT(17, 1);
-            if (fast) {
-                if (in.pos != NU || in.neg != NL) { ok = false; break; }
-            } else {
-                in = bk_factor_fixed<LDK, NK>(Ks, perm, piv);
-                if (in.zero) { ok = false; zero = true; break; }
-                if (in.pos != NU || in.neg != NL) { ok = false; break; }
-                bk_solve_cols<LDK, NRK, NK>(Ks, perm, piv, Rk, NRK);
+            STAMP_COUNT(16, nsr < 0 ? 1 : 0);
+            if (nsr == 0) { ok = false; break; }
+            if (nsr < 0) {
+                // ---- stage block [[Quu, Du^T], [Du, -dc]] and right-hand sides -[Qux | qu ; G | e]
+                // Block rows order the controls as (F, qd): with active torque bounds the force
+                // carries the large curvature Sigma_s (J^T F)^2 and the joint velocities couple to it
+                // weakly, so natural-order 1x1 pivots pass the Bunch-Kaufman test (ldl_schur_regs).
+                // uo(a): control index (qd 0..n-1, F n..) of block row a < NU.
+                for (int e = lane; e < NK * NK; e += 64) {
+                    int a = e / NK, c = e % NK;
+                    double val;
+                    if (a < NU && c < NU) {
+                        const int ua = uo(a), uc = uo(c);
+                        val = Hs[(n + ua) * NV + n + uc];
+                        if (ua < n && uc < n) val += h * h * Ps[ua * n + uc];
+                    } else if (a >= NU && c >= NU) {
+                        val = (a == c) ? (con ? -dc : -1.0) : 0.0;
+                    } else {
+                        int l = (a >= NU) ? a - NU : c - NU, v = uo((a >= NU) ? c : a);
+                        val = (con && v < n) ? h * Gl[l * n + v] : 0.0;
+                    }
+                    Ks[a * LDK + c] = val;
+                }
+                for (int e = lane; e < NK * NRK; e += 64) {
+                    int a = e / NRK, c = e % NRK;
+                    double val;
+                    if (a < NU) {
+                        const int ua = uo(a);
+                        if (c < n) val = -(Hs[(n + ua) * NV + c] + (ua < n ? h * Ps[ua * n + c] : 0.0));
+                        else val = -(gsk[n + ua] + (ua < n ? h * ss[ua] : 0.0));
+                    } else {
+                        int l = a - NU;
+                        val = con ? -(c < n ? Gl[l * n + c] : elk[l]) : 0.0;
+                    }
+                    Rk[e] = val;
+                }
+                wave_lds_sync();
+                STAMP(12);
+                BKInertia in;
+                const bool fast = ldl_schur_regs<LDK, NRK, NU, NL>(Ks, Rk, NRK, in);
+                STAMP(13);
+                if (fast) {
+                    if (in.pos != NU || in.neg != NL) { ok = false; break; }
+                } else {
+                    in = bk_factor_fixed<LDK, NK>(Ks, perm, piv);
+                    if (in.zero) { ok = false; zero = true; break; }
+                    if (in.pos != NU || in.neg != NL) { ok = false; break; }
+                    bk_solve_cols<LDK, NRK, NK>(Ks, perm, piv, Rk, NRK);
+                }
             }
             STAMP(14);
             // ---- P_k = Qxx + Qxu Ku + G^T Kl ; p_k = qx + Qxu ku + G^T kl   (block row a <-> control uo(a))
@@ -868,70 +1017,81 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     // ---------------- forward sweep: du_k = Ku dx_k + ku, dyl_{k+1} = Kl dx_k + kl,
     //                  dyc_k = P_{k+1} dx_{k+1} + p_{k+1} + Jl_{k+1}^T dyl_{k+1}
     // (the node-(k+1) line constraint was pushed back onto stage k, so V_{k+1} does not contain
-    // it but the q_{k+1} row of the KKT does).  Slot k+1 is prefetched while stage k runs.
-    double sr[NSR];
-#pragma unroll
-    for (int t = 0; t < NSR; t++) {
-        const int e = lane + 64 * t;
-        sr[t] = (e < SLOT) ? ((e < MB * NJ) ? G[e] : wv[e - MB * NJ]) : 0.0;  // slot 0
-    }
-    for (int j = lane; j < n; j += 64) {
-        dq[j] = 0.0; dqd[j] = 0.0;
-        xs[j] = cst[j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
-    }
-    for (int l = lane; l < nl; l += 64) { dyl[l] = 0.0; dyl[nl + l] = 0.0; }
-    for (int k = 0; k < N; k++) {
-        // slot k -> LDS; prefetch slot k+1
+    // it but the q_{k+1} row of the KKT does).  Slots and Jl_{k+1} are prefetched FD stages
+    // ahead into a register ring (a stage is shorter than one global-memory round trip).
+    constexpr int FD = 4;
+    constexpr int NGL = NL > 0 ? NL * NJ : 1;
+    double sr[FD][NSR], glr_f[FD], cr_f[FD];
+    auto fetch = [&](int kk, double *srr, double &g, double &cr) {
+        const double *Gn = G + (size_t)kk * MB * n, *wn = wv + (size_t)kk * MB;
 #pragma unroll
         for (int t = 0; t < NSR; t++) {
             const int e = lane + 64 * t;
-            if (e < SLOT) Sl[e] = sr[t];
+            srr[t] = (e < SLOT) ? ((e < MB * NJ) ? Gn[e] : wn[e - MB * NJ]) : 0.0;
         }
-        if (k + 1 < N) {
-            const double *Gn = G + (size_t)(k + 1) * MB * n, *wn = wv + (size_t)(k + 1) * MB;
+        g = (NL > 0 && lane < NGL && kk + 1 < N) ? Jl[(size_t)(kk + 1) * NGL + lane] : 0.0;
+        cr = (lane < NJ) ? stg[(size_t)kk * SG + NV + lane] : 0.0;  // c_k
+    };
+#pragma unroll
+    for (int r = 0; r < FD; r++)
+        if (r < N) fetch(r, sr[r], glr_f[r], cr_f[r]);
+    for (int j = lane; j < n; j += 64) {
+        dq[j] = 0.0; dqd[j] = 0.0;
+        xs[j] = stg[NV + j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
+    }
+    for (int l = lane; l < nl; l += 64) { dyl[l] = 0.0; dyl[nl + l] = 0.0; }
+    for (int k0 = 0; k0 < N; k0 += FD) {
+#pragma unroll
+        for (int r = 0; r < FD; r++) {
+            const int k = k0 + r;
+            if (k >= N) break;
+            // slot k -> LDS; prefetch slot k + FD into the freed ring entry
 #pragma unroll
             for (int t = 0; t < NSR; t++) {
                 const int e = lane + 64 * t;
-                sr[t] = (e < SLOT) ? ((e < MB * NJ) ? Gn[e] : wn[e - MB * NJ]) : 0.0;
+                if (e < SLOT) Sl[e] = sr[r][t];
             }
-        }
-        wave_lds_sync();
-        const double *Gk = Sl, *wk = Sl + MB * NJ;
-        if (k == 0) {
-            for (int a = lane; a < nf; a += 64) dF[a] = wk[NJ + a];
-            for (int j = lane; j < n; j += 64) {  // dyc_0 = P_1 dx_1 + p_1 (stage-1 line is masked)
+            if (lane < NGL) Gl[lane] = glr_f[r];
+            if (lane < NJ) Stg[lane] = cr_f[r];
+            if (k + FD < N) fetch(k + FD, sr[r], glr_f[r], cr_f[r]);
+            wave_lds_sync();
+            const double *Gk = Sl, *wk = Sl + MB * NJ;
+            if (k == 0) {
+                for (int a = lane; a < nf; a += 64) dF[a] = wk[NJ + a];
+                for (int j = lane; j < n; j += 64) {  // dyc_0 = P_1 dx_1 + p_1 (stage-1 line is masked)
+                    double a = wk[NU + NL + j];
+                    for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * xs[i];
+                    dyc[j] = a;
+                }
+                wave_lds_sync();
+                continue;
+            }
+            for (int a = lane; a < NK; a += 64) {
+                double v = wk[a];
+                for (int i = 0; i < n; i++) v += Gk[a * n + i] * xs[i];
+                us[a] = v;
+            }
+            for (int j = lane; j < n; j += 64) dq[k * n + j] = xs[j];
+            wave_lds_sync();
+            for (int j = lane; j < n; j += 64) {
+                dqd[k * n + j] = us[j];
+                cs[j] = xs[j] + h * us[j] + Stg[j];
+            }
+            for (int a = lane; a < nf; a += 64) dF[k * NFA + a] = us[NJ + a];
+            const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
+            if (k + 1 < N)
+                for (int l = lane; l < nl; l += 64) dyl[(k + 1) * nl + l] = con1 ? us[NU + l] : 0.0;
+            wave_lds_sync();
+            for (int j = lane; j < n; j += 64) {
                 double a = wk[NU + NL + j];
-                for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * xs[i];
-                dyc[j] = a;
+                for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * cs[i];
+                if (con1)
+                    for (int l = 0; l < nl; l++) a += Gl[l * n + j] * us[NU + l];
+                dyc[k * n + j] = a;
+                xs[j] = cs[j];
             }
             wave_lds_sync();
-            continue;
         }
-        for (int a = lane; a < NK; a += 64) {
-            double v = wk[a];
-            for (int i = 0; i < n; i++) v += Gk[a * n + i] * xs[i];
-            us[a] = v;
-        }
-        for (int j = lane; j < n; j += 64) dq[k * n + j] = xs[j];
-        wave_lds_sync();
-        for (int j = lane; j < n; j += 64) {
-            dqd[k * n + j] = us[j];
-            cs[j] = xs[j] + h * us[j] + cst[k * n + j];
-        }
-        for (int a = lane; a < nf; a += 64) dF[k * NFA + a] = us[NJ + a];
-        const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
-        if (k + 1 < N)
-            for (int l = lane; l < nl; l += 64) dyl[(k + 1) * nl + l] = con1 ? us[NU + l] : 0.0;
-        wave_lds_sync();
-        for (int j = lane; j < n; j += 64) {
-            double a = wk[NU + NL + j];
-            for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * cs[i];
-            if (con1)
-                for (int l = 0; l < nl; l++) a += Jl[((size_t)(k + 1) * nl + l) * n + j] * us[NU + l];
-            dyc[k * n + j] = a;
-            xs[j] = cs[j];
-        }
-        wave_lds_sync();
     }
     for (int j = lane; j < n; j += 64) dq[N * n + j] = xs[j];
     __threadfence_block();
@@ -939,43 +1099,85 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
 
     // ---------------- dyd, ds, dz, dv
     double pcorr = 0.0;  // sum Sigma_s (ds^2 - (J dx)^2): turns p^T H0 p into the oracle's p^T (W + Sigma) p
-    for (int e = lane; e < N * n; e += 64) {
-        int k = e / n, j = e % n, i = e;
-        if (!TACT(k, j)) { dyd[i] = 0.0; ds[i] = 0.0; continue; }
-        const double *Jtk = Jt + (size_t)k * n * NV;
-        double jdx = 0.0;
-        for (int u = 0; u < n; u++) jdx += Jtk[j * NV + u] * dq[k * n + u] + Jtk[j * NV + n + u] * dqd[k * n + u];
-        for (int a = 0; a < nf; a++) jdx += Jtk[j * NV + 2 * n + a] * dF[k * NFA + a];
-        double sg = Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
-        double rs = gphs[i] - yd[i], rd = tau[i] - s[i];
-        dyd[i] = Dd * (jdx + rd + rs / sg);
-        ds[i] = (dyd[i] - rs) / sg;
-        pcorr += Ss[i] * (ds[i] * ds[i] - jdx * jdx);
-    }
-    for (int e = lane; e < (N + 1) * n; e += 64) {
-        int k = e / n, j = e % n;
-        double a = 0, bb = 0;
-        if (k > 0) {
-            double x = q[e], dx = dq[e];
-            if (hasb(QLO[j])) a = mu / (x - QLO[j]) - zqL[e] - zqL[e] / (x - QLO[j]) * dx;
-            if (hasb(QHI[j])) bb = mu / (QHI[j] - x) - zqU[e] + zqU[e] / (QHI[j] - x) * dx;
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        double jdx[UB], ssv[UB], gv[UB], ydv[UB], tv[UB], sv[UB], lo[UB], hi[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            const int k = e / n, j = e % n;
+            const double *Jtk = Jt + ((size_t)k * n + j) * NV;
+            double a = 0.0;
+#pragma unroll
+            for (int v = 0; v < NJ; v++) a += Jtk[v] * dq[k * n + v] + Jtk[n + v] * dqd[k * n + v];
+#pragma unroll
+            for (int f = 0; f < NF; f++) a += Jtk[2 * n + f] * dF[k * NFA + f];
+            jdx[u] = a;
+            ssv[u] = Ss[e]; gv[u] = gphs[e]; ydv[u] = yd[e]; tv[u] = tau[e]; sv[u] = s[e];
+            lo[u] = tlo[e]; hi[u] = thi[e];
         }
-        dzqL[e] = a; dzqU[e] = bb;
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * n) {
+                double dydv = 0.0, dsv = 0.0;
+                if (hasb(lo[u]) || hasb(hi[u])) {
+                    const double sg = ssv[u] + dw, Dd = sg / (1.0 + dc * sg);
+                    const double rs = gv[u] - ydv[u], rd = tv[u] - sv[u];
+                    dydv = Dd * (jdx[u] + rd + rs / sg);
+                    dsv = (dydv - rs) / sg;
+                    pcorr += ssv[u] * (dsv * dsv - jdx[u] * jdx[u]);
+                }
+                dyd[e] = dydv;
+                ds[e] = dsv;
+            }
+        }
+    }
+    for (int e0 = lane; e0 < (N + 1) * n; e0 += 64 * UB) {
+        double x[UB], dx[UB], zl[UB], zu[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, (N + 1) * n - 1);
+            x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; zu[u] = zqU[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < (N + 1) * n) {
+                const int k = e / n, j = e % n;
+                double a = 0, bb = 0;
+                if (k > 0) {
+                    if (hasb(QLO[j])) a = mu / (x[u] - QLO[j]) - zl[u] - zl[u] / (x[u] - QLO[j]) * dx[u];
+                    if (hasb(QHI[j])) bb = mu / (QHI[j] - x[u]) - zu[u] + zu[u] / (QHI[j] - x[u]) * dx[u];
+                }
+                dzqL[e] = a; dzqU[e] = bb;
+            }
+        }
     }
     __threadfence_block();
     __syncthreads();
-    for (int e = lane; e < N * n; e += 64) {
-        int k = e / n, j = e % n;
-        double a = 0, bb = 0, c = 0, d = 0;
-        if (k > 0) {
-            double x = qd[e], dx = dqd[e];
-            if (hasb(DLO[j])) a = mu / (x - DLO[j]) - zdL[e] - zdL[e] / (x - DLO[j]) * dx;
-            if (hasb(DHI[j])) bb = mu / (DHI[j] - x) - zdU[e] + zdU[e] / (DHI[j] - x) * dx;
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        double x[UB], dx[UB], zl[UB], zu[UB], xs[UB], dxs[UB], vl[UB], vu[UB], lo[UB], hi[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            x[u] = qd[e]; dx[u] = dqd[e]; zl[u] = zdL[e]; zu[u] = zdU[e];
+            xs[u] = s[e]; dxs[u] = ds[e]; vl[u] = vL[e]; vu[u] = vU[e]; lo[u] = tlo[e]; hi[u] = thi[e];
         }
-        double x = s[e], dx = ds[e];
-        if (hasb(tlo[e])) c = mu / (x - tlo[e]) - vL[e] - vL[e] / (x - tlo[e]) * dx;
-        if (hasb(thi[e])) d = mu / (thi[e] - x) - vU[e] + vU[e] / (thi[e] - x) * dx;
-        dzdL[e] = a; dzdU[e] = bb; dvL[e] = c; dvU[e] = d;
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * n) {
+                const int k = e / n, j = e % n;
+                double a = 0, bb = 0, c = 0, d = 0;
+                if (k > 0) {
+                    if (hasb(DLO[j])) a = mu / (x[u] - DLO[j]) - zl[u] - zl[u] / (x[u] - DLO[j]) * dx[u];
+                    if (hasb(DHI[j])) bb = mu / (DHI[j] - x[u]) - zu[u] + zu[u] / (DHI[j] - x[u]) * dx[u];
+                }
+                if (hasb(lo[u])) c = mu / (xs[u] - lo[u]) - vl[u] - vl[u] / (xs[u] - lo[u]) * dxs[u];
+                if (hasb(hi[u])) d = mu / (hi[u] - xs[u]) - vu[u] + vu[u] / (hi[u] - xs[u]) * dxs[u];
+                dzdL[e] = a; dzdU[e] = bb; dvL[e] = c; dvU[e] = d;
+            }
+        }
     }
     __threadfence_block();
     __syncthreads();
@@ -986,32 +1188,67 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
     auto ftbL = [&](double x, double dx, double lo, double &a) { if (dx < 0) a = fmin(a, -tau_fb * (x - lo) / dx); };
     auto ftbU = [&](double x, double dx, double hi, double &a) { if (dx > 0) a = fmin(a, tau_fb * (hi - x) / dx); };
     auto ftbZ = [&](double z, double dz, double &a) { if (dz < 0) a = fmin(a, -tau_fb * z / dz); };
-    for (int e = n + lane; e < (N + 1) * n; e += 64) {
-        int j = e % n;
-        if (hasb(QLO[j])) { ftbL(q[e], dq[e], QLO[j], ap); ftbZ(zqL[e], dzqL[e], az); }
-        if (hasb(QHI[j])) { ftbU(q[e], dq[e], QHI[j], ap); ftbZ(zqU[e], dzqU[e], az); }
-    }
-    for (int e = lane; e < N * n; e += 64) {
-        int k = e / n, j = e % n;
-        if (k > 0) {
-            if (hasb(DLO[j])) { ftbL(qd[e], dqd[e], DLO[j], ap); ftbZ(zdL[e], dzdL[e], az); }
-            if (hasb(DHI[j])) { ftbU(qd[e], dqd[e], DHI[j], ap); ftbZ(zdU[e], dzdU[e], az); }
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {  // q_k, k = 1..N
+        double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1) + n;
+            x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; dzl[u] = dzqL[e]; zu[u] = zqU[e]; dzu[u] = dzqU[e];
         }
-        if (hasb(tlo[e])) { ftbL(s[e], ds[e], tlo[e], ap); ftbZ(vL[e], dvL[e], az); }
-        if (hasb(thi[e])) { ftbU(s[e], ds[e], thi[e], ap); ftbZ(vU[e], dvU[e], az); }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            if (e0 + 64 * u < N * n) {
+                const int j = (e0 + 64 * u) % n;
+                if (hasb(QLO[j])) { ftbL(x[u], dx[u], QLO[j], ap); ftbZ(zl[u], dzl[u], az); }
+                if (hasb(QHI[j])) { ftbU(x[u], dx[u], QHI[j], ap); ftbZ(zu[u], dzu[u], az); }
+            }
+        }
+    }
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB], xs[UB], dxs[UB], vl[UB], dvl[UB], vu[UB], dvu[UB], lo[UB], hi[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            x[u] = qd[e]; dx[u] = dqd[e]; zl[u] = zdL[e]; dzl[u] = dzdL[e]; zu[u] = zdU[e]; dzu[u] = dzdU[e];
+            xs[u] = s[e]; dxs[u] = ds[e]; vl[u] = vL[e]; dvl[u] = dvL[e]; vu[u] = vU[e]; dvu[u] = dvU[e];
+            lo[u] = tlo[e]; hi[u] = thi[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * n) {
+                const int k = e / n, j = e % n;
+                if (k > 0) {
+                    if (hasb(DLO[j])) { ftbL(x[u], dx[u], DLO[j], ap); ftbZ(zl[u], dzl[u], az); }
+                    if (hasb(DHI[j])) { ftbU(x[u], dx[u], DHI[j], ap); ftbZ(zu[u], dzu[u], az); }
+                }
+                if (hasb(lo[u])) { ftbL(xs[u], dxs[u], lo[u], ap); ftbZ(vl[u], dvl[u], az); }
+                if (hasb(hi[u])) { ftbU(xs[u], dxs[u], hi[u], ap); ftbZ(vu[u], dvu[u], az); }
+            }
+        }
     }
     ap = wave_min(ap);
     az = wave_min(az);
     TRACE(9, ap); TRACE(10, az);
 
     // ---------------- merit at the current point, directional derivative, curvature
-    // merit of a point (x + alpha dx); alpha = 0 uses the stored node values
+    // merit of a point (x + alpha dx).  Each lane sweeps its nodes with node_values; the node's
+    // iterate and step are loaded into registers before the sweep starts.
     const int fpj = (NF > 0 || NL > 0) ? F.parent : -1;
     auto merit = [&](double alpha, double &phi, double &theta, bool &ok_out) {
         double f = 0, bar = 0, th = 0;
         int bad = 0;
         for (int k = lane; k < N; k += 64) {
-            double Fw[3], c = 0.0;
+            double tq[NJ], tqd[NJ], qn[NJ], sl[NJ], lo[NJ], hi[NJ], Fw[3], c = 0.0;
+#pragma unroll
+            for (int j = 0; j < NJ; j++) {
+                tq[j] = q[k * n + j] + alpha * dq[k * n + j];
+                tqd[j] = qd[k * n + j] + alpha * dqd[k * n + j];
+                qn[j] = q[(k + 1) * n + j] + alpha * dq[(k + 1) * n + j];
+                sl[j] = s[k * n + j] + alpha * ds[k * n + j];
+                lo[j] = tlo[k * n + j];
+                hi[j] = thi[k * n + j];
+            }
 #pragma unroll
             for (int r = 0; r < 3; r++) Fw[r] = 0.0;
 #pragma unroll
@@ -1021,36 +1258,57 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
 #pragma unroll
                 for (int r = 0; r < 3; r++) Fw[r] += tF * C.fdir[3 * a + r];
             }
-            TrialIn tin{q + (size_t)k * n, dq + (size_t)k * n, qd + (size_t)k * n, dqd + (size_t)k * n, alpha};
-            MeritOut mo{s + (size_t)k * n, ds + (size_t)k * n, tlo + (size_t)k * n, thi + (size_t)k * n, lref,
-                        alpha, C.wtau, 0.0, 0.0, nl, LINE_ON(k)};
+            struct MOut {
+                const double *sl, *lo, *hi, *lref;
+                double wtau, c, th;
+                int nl;
+                bool line;
+                __device__ void frame(const double *p) {
+                    if (line)
+                        for (int l = 0; l < nl; l++) th += fabs(p[l] - lref[l]);
+                }
+                __device__ void force(const double *) {}
+                __device__ void joint(int j, double t, double, double) {
+                    c += wtau * t * t;
+                    if (hasb(lo[j]) || hasb(hi[j])) th += fabs(t - sl[j]);
+                }
+            } mo{sl, lo, hi, lref, C.wtau, 0.0, 0.0, nl, LINE_ON(k)};
+            ArrIn<NJ> tin{tq, tqd};
             node_values<NJ>(M, F, fpj, tin, Fw, mo);
 #pragma unroll
             for (int j = 0; j < NJ; j++) {
-                const double tq = q[k * n + j] + alpha * dq[k * n + j], tqd = qd[k * n + j] + alpha * dqd[k * n + j];
-                const double qn = q[(k + 1) * n + j] + alpha * dq[(k + 1) * n + j];
-                c += C.wqd * tqd * tqd;
-                th += fabs(tq + h * tqd - qn);
+                c += C.wqd * tqd[j] * tqd[j];
+                th += fabs(tq[j] + h * tqd[j] - qn[j]);
             }
             f += c + mo.c;
             th += mo.th;
         }
-        for (int e = n + lane; e < (N + 1) * n; e += 64) {
-            int j = e % n;
-            double x = q[e] + alpha * dq[e];
-            if (hasb(QLO[j])) { if (x - QLO[j] <= 0) bad = 1; else bar -= log(x - QLO[j]); }
-            if (hasb(QHI[j])) { if (QHI[j] - x <= 0) bad = 1; else bar -= log(QHI[j] - x); }
-        }
-        for (int e = lane; e < N * n; e += 64) {
-            int k = e / n, j = e % n;
-            if (k > 0) {
-                double x = qd[e] + alpha * dqd[e];
-                if (hasb(DLO[j])) { if (x - DLO[j] <= 0) bad = 1; else bar -= log(x - DLO[j]); }
-                if (hasb(DHI[j])) { if (DHI[j] - x <= 0) bad = 1; else bar -= log(DHI[j] - x); }
+        for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+            double xq[UB], xd[UB], xs[UB], lo[UB], hi[UB];
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = min(e0 + 64 * u, N * n - 1);
+                xq[u] = q[e + n] + alpha * dq[e + n];
+                xd[u] = qd[e] + alpha * dqd[e];
+                xs[u] = s[e] + alpha * ds[e];
+                lo[u] = tlo[e];
+                hi[u] = thi[e];
             }
-            double x = s[e] + alpha * ds[e];
-            if (hasb(tlo[e])) { if (x - tlo[e] <= 0) bad = 1; else bar -= log(x - tlo[e]); }
-            if (hasb(thi[e])) { if (thi[e] - x <= 0) bad = 1; else bar -= log(thi[e] - x); }
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = e0 + 64 * u;
+                if (e < N * n) {
+                    const int k = e / n, j = e % n;
+                    if (hasb(QLO[j])) { if (xq[u] - QLO[j] <= 0) bad = 1; else bar -= log(xq[u] - QLO[j]); }
+                    if (hasb(QHI[j])) { if (QHI[j] - xq[u] <= 0) bad = 1; else bar -= log(QHI[j] - xq[u]); }
+                    if (k > 0) {
+                        if (hasb(DLO[j])) { if (xd[u] - DLO[j] <= 0) bad = 1; else bar -= log(xd[u] - DLO[j]); }
+                        if (hasb(DHI[j])) { if (DHI[j] - xd[u] <= 0) bad = 1; else bar -= log(DHI[j] - xd[u]); }
+                    }
+                    if (hasb(lo[u])) { if (xs[u] - lo[u] <= 0) bad = 1; else bar -= log(xs[u] - lo[u]); }
+                    if (hasb(hi[u])) { if (hi[u] - xs[u] <= 0) bad = 1; else bar -= log(hi[u] - xs[u]); }
+                }
+            }
         }
         f = wave_sum(f); bar = wave_sum(bar); th = wave_sum(th);
         bad = wave_sum_i(bad);
@@ -1065,21 +1323,46 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         bool ok0;
         merit(0.0, phi0, th0, ok0);
     }
+    // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx; lane e covers row v of node k's W
     double gdot = 0, pHp = pcorr;
-    for (int k = lane; k < N; k += 64) {
-        const double *Wk = W + (size_t)k * NV * NV;
-        double dx[NV];
-        for (int j = 0; j < n; j++) { dx[j] = dq[k * n + j]; dx[n + j] = dqd[k * n + j]; }
-        for (int a = 0; a < nf; a++) dx[2 * n + a] = dF[k * NFA + a];
-        for (int u = 0; u < NV; u++) {
-            gdot += gf[k * NV + u] * dx[u];
-            for (int v = 0; v < NV; v++) pHp += dx[u] * Wk[u * NV + v] * dx[v];
+    for (int e0 = lane; e0 < N * NV; e0 += 64 * 2) {
+        double acc[2], gd[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int e = min(e0 + 64 * u, N * NV - 1);
+            const int k = e / NV, v = e % NV;
+            double dx[NV];
+#pragma unroll
+            for (int j = 0; j < NJ; j++) { dx[j] = dq[k * n + j]; dx[NJ + j] = dqd[k * n + j]; }
+#pragma unroll
+            for (int a = 0; a < NF; a++) dx[2 * NJ + a] = dF[k * NFA + a];
+            const double *Wr = W + (size_t)k * NV * NV + (size_t)v * NV;
+            double a = 0.0, dv = 0.0;
+#pragma unroll
+            for (int w = 0; w < NV; w++) {
+                a += Wr[w] * dx[w];
+                if (w == v) dv = dx[w];
+            }
+            acc[u] = a * dv;
+            gd[u] = gf[e] * dv;
         }
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            if (e0 + 64 * u < N * NV) { pHp += acc[u]; gdot += gd[u]; }
     }
-    for (int e = lane; e < N * n; e += 64) gdot += gphd[e] * dqd[e] + gphs[e] * ds[e];
-    for (int e = n + lane; e < (N + 1) * n; e += 64) {
-        gdot += gphq[e] * dq[e];
-        if (e >= N * n) pHp += Sxq[e] * dq[e] * dq[e];  // q_N (stages k < N carry Sigma_x in H0)
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        double g1[UB], g2[UB], g3[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            const double dqv = dq[e + n];
+            g1[u] = gphd[e] * dqd[e] + gphs[e] * ds[e];
+            g2[u] = gphq[e + n] * dqv;
+            g3[u] = (e + n >= N * n) ? Sxq[e + n] * dqv * dqv : 0.0;  // q_N (stages k < N carry Sigma_x in H0)
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++)
+            if (e0 + 64 * u < N * n) { gdot += g1[u] + g2[u]; pHp += g3[u]; }
     }
     gdot = wave_sum(gdot);
     pHp = wave_sum(pHp);
@@ -1116,35 +1399,65 @@ __global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg
         st.consec_fail = 0;
     }
 
-    // ---------------- update
-    for (int e = lane; e < (N + 1) * n; e += 64) q[e] += alpha * dq[e];
-    for (int e = lane; e < N * n; e += 64) {
-        qd[e] += alpha * dqd[e]; s[e] += alpha * ds[e];
-        yc[e] += alpha * dyc[e]; yd[e] += alpha * dyd[e];
+    // ---------------- update (primal-dual step, then the bound multipliers with the new slacks)
+    auto zupd = [&](double z, double dz, double slack) {
+        const double zz = z + az * dz;
+        return fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
+    };
+    for (int e0 = lane; e0 < (N + 1) * n; e0 += 64 * UB) {
+        double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, (N + 1) * n - 1);
+            x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; dzl[u] = dzqL[e]; zu[u] = zqU[e]; dzu[u] = dzqU[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < (N + 1) * n) {
+                const int j = e % n;
+                const double xn = x[u] + alpha * dx[u];
+                q[e] = xn;
+                if (e >= n) {
+                    if (hasb(QLO[j])) zqL[e] = zupd(zl[u], dzl[u], xn - QLO[j]);
+                    if (hasb(QHI[j])) zqU[e] = zupd(zu[u], dzu[u], QHI[j] - xn);
+                }
+            }
+        }
+    }
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        double x[UB], xs[UB], zl[UB], zu[UB], vl[UB], vu[UB], lo[UB], hi[UB], yn[UB], dn[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            x[u] = qd[e] + alpha * dqd[e];
+            xs[u] = s[e] + alpha * ds[e];
+            yn[u] = yc[e] + alpha * dyc[e];
+            dn[u] = yd[e] + alpha * dyd[e];
+            zl[u] = zdL[e] + az * dzdL[e]; zu[u] = zdU[e] + az * dzdU[e];
+            vl[u] = vL[e] + az * dvL[e]; vu[u] = vU[e] + az * dvU[e];
+            lo[u] = tlo[e]; hi[u] = thi[e];
+        }
+        auto clampz = [&](double zz, double slack) {
+            return fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
+        };
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + 64 * u;
+            if (e < N * n) {
+                const int k = e / n, j = e % n;
+                qd[e] = x[u]; s[e] = xs[u]; yc[e] = yn[u]; yd[e] = dn[u];
+                if (k > 0) {
+                    if (hasb(DLO[j])) zdL[e] = clampz(zl[u], x[u] - DLO[j]);
+                    if (hasb(DHI[j])) zdU[e] = clampz(zu[u], DHI[j] - x[u]);
+                }
+                if (hasb(lo[u])) vL[e] = clampz(vl[u], xs[u] - lo[u]);
+                if (hasb(hi[u])) vU[e] = clampz(vu[u], hi[u] - xs[u]);
+            }
+        }
     }
     for (int e = lane; e < N * nf; e += 64) Fv[(e / nf) * NFA + e % nf] += alpha * dF[(e / nf) * NFA + e % nf];
     for (int e = lane; e < N * nl; e += 64) yl[e] += alpha * dyl[e];
-    __threadfence_block();
-    __syncthreads();
-    auto zupd = [&](double &z, double dz, double slack) {
-        double zz = z + az * dz;
-        zz = fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
-        z = zz;
-    };
-    for (int e = n + lane; e < (N + 1) * n; e += 64) {
-        int j = e % n;
-        if (hasb(QLO[j])) zupd(zqL[e], dzqL[e], q[e] - QLO[j]);
-        if (hasb(QHI[j])) zupd(zqU[e], dzqU[e], QHI[j] - q[e]);
-    }
-    for (int e = lane; e < N * n; e += 64) {
-        int k = e / n, j = e % n;
-        if (k > 0) {
-            if (hasb(DLO[j])) zupd(zdL[e], dzdL[e], qd[e] - DLO[j]);
-            if (hasb(DHI[j])) zupd(zdU[e], dzdU[e], DHI[j] - qd[e]);
-        }
-        if (hasb(tlo[e])) zupd(vL[e], dvL[e], s[e] - tlo[e]);
-        if (hasb(thi[e])) zupd(vU[e], dvU[e], thi[e] - s[e]);
-    }
     STAMP(6);
     STAMP_COUNT(10, 1);
     STAMP_FLUSH;
@@ -1206,17 +1519,8 @@ struct IpmLaunch {
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3((unsigned)((nodes + NPB - 1) / NPB)), dim3(256), 0, s,
                                M, F, C, A, batch);
         else {
-            const size_t dyn = ipm_dyn_lds(C.N);
-            if (dyn > 64 * 1024)
-                (void)hipFuncSetAttribute((const void *)k_ipm_iter<NJ, NF, NL>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
-            hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), dyn, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
         }
-    }
-    // dynamic LDS of k_ipm_iter: per-stage g_k (NV), c_k (NJ), e_k (NL), y_tau + D r_tau (NJ), dD (NJ)
-    static size_t ipm_dyn_lds(int N) {
-        constexpr int NV = 2 * NJ + NF;
-        return (size_t)N * (NV + 3 * NJ + (NL > 0 ? NL : 1)) * sizeof(double);
     }
     static void output(const OcpConst &C, const IpmArrays &A, int batch, double *w, int *status, int *iters,
                        double *kkt, double *obj, hipStream_t s) {

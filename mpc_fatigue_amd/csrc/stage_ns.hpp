@@ -1,0 +1,173 @@
+// Null-space solve of one Riccati stage block.
+//
+// Stage k of the backward recursion solves
+//     [ Q  D^T ] [u]   [b_u]        Q = Q_uu (NU x NU), controls u = (qd_0..qd_{NJ-1}, F_0..),
+//     [ D   0  ] [l] = [b_l]        D = h Jl_{k+1} on the qd columns, 0 on the force columns,
+// for NJ + 1 right-hand sides (the NJ columns of -[Q_ux; Jl_{k+1}] and -[q_u; e_k]), and
+// must report whether the block has inertia (NU, 2).  The pivoted Bunch-Kaufman path
+// (bk_wave.hpp) does this with nine dependent pivot steps, each a cross-lane exchange.
+// Here the two constraint rows are eliminated first, through a 2 x 2 block D_J of D
+// picked by partial pivoting (columns j1, j2 of the joint velocities):
+//     Z = [ -D_J^{-1} D_R ; I ]  (NU x NR, NR = NU - 2, R = the other controls)
+// spans null(D).  With the block pivot [[Q_JJ, D_J^T], [D_J, 0]] (inertia (2, 2) for any
+// invertible D_J) Haynsworth additivity gives
+//     inertia(K) = (2, 2) + inertia(Z^T Q Z),
+// so K has inertia (NU, 2) exactly when the reduced Hessian S = Z^T Q Z (NR x NR) is
+// positive definite, i.e. when its LDL^T without pivoting has positive pivots.  That is
+// the same exact test as the pivoted factorisation of K, with a fixed elimination order:
+//   * 25 lanes form S entry-wise from LDS reads of the stage Hessian and P (one round);
+//   * every lane factors S redundantly in registers (no cross-lane traffic);
+//   * lane c solves right-hand side c:  u_p = D_J^{-1} b_l on J, u_R = S^{-1} Z^T (b_u - Q u_p),
+//     u_J = u_p,J + Z_JR u_R,  l = D_J^{-T} (b_u,J - (Q u)_J).
+// Degenerate constraint blocks (D_J numerically singular) and dc > 0 stay with the pivoted
+// path (the caller decides).  The result lands in Rk in the pivoted path's block-row order
+// (force rows first, then joint velocities, then the two multipliers).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace mf {
+
+// returns 1: solved, inertia (NU, 2); 0: wrong inertia; -1: degenerate (use the pivoted path)
+template <int NJ, int NF, int NV, int NRK>
+__device__ __forceinline__ int stage_nullspace(const double *Hs, const double *Ps, const double *ss, const double *Gl,
+                                               const double *gsk, const double *elk, double h, double *Ss5,
+                                               double *Rk) {
+    constexpr int NU = NJ + NF, NR = NU - 2;
+    const int lane = threadIdx.x;
+    const double hh = h * h;
+    // Q entry (controls x, y; x, y < NJ are joint velocities)
+    auto Qe = [&](int x, int y) {
+        double v = Hs[(NJ + x) * NV + NJ + y];
+        if (x < NJ && y < NJ) v += hh * Ps[x * NJ + y];
+        return v;
+    };
+    auto Dc = [&](int l, int x) { return x < NJ ? h * Gl[l * NJ + x] : 0.0; };
+    // ---- pivot columns of D (partial pivoting; ties keep the smallest index)
+    int j1 = 0;
+    double m1 = fabs(h * Gl[0]);
+#pragma unroll
+    for (int j = 1; j < NJ; j++) {
+        const double a = fabs(h * Gl[j]);
+        if (a > m1) { m1 = a; j1 = j; }
+    }
+    const double d0j1 = h * Gl[j1], d1j1 = h * Gl[NJ + j1];
+    int j2 = -1;
+    double m2 = 0.0;
+    if (m1 > 0.0) {
+        const double f = d1j1 / d0j1;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            if (j == j1) continue;
+            const double a = fabs(h * Gl[NJ + j] - f * (h * Gl[j]));
+            if (a > m2) { m2 = a; j2 = j; }
+        }
+    }
+    if (!(m1 > 0.0) || j2 < 0 || !(m2 > 1e-10 * m1)) return -1;
+    const int J0 = j1, J1 = j2;
+    const double a00 = d0j1, a01 = h * Gl[J1], a10 = d1j1, a11 = h * Gl[NJ + J1];
+    const double det = a00 * a11 - a01 * a10;
+    const double i00 = a11 / det, i01 = -a01 / det, i10 = -a10 / det, i11 = a00 / det;  // D_J^{-1}
+    const int lo = J0 < J1 ? J0 : J1, hi = J0 < J1 ? J1 : J0;
+    auto Ridx = [&](int m) {
+        if (m >= NJ - 2) return NJ + (m - (NJ - 2));  // force controls
+        int x = m;
+        if (x >= lo) x++;
+        if (x >= hi) x++;
+        return x;
+    };
+    // Z_JR column m: -D_J^{-1} D[:, R_m]
+    auto Zc = [&](int m, double &z0, double &z1) {
+        const int x = Ridx(m);
+        const double e0 = Dc(0, x), e1 = Dc(1, x);
+        z0 = -(i00 * e0 + i01 * e1);
+        z1 = -(i10 * e0 + i11 * e1);
+    };
+    // ---- reduced Hessian S = Z^T Q Z, one entry per lane
+    if (lane < NR * NR) {
+        const int a = lane / NR, b = lane % NR;
+        const int Ra = Ridx(a), Rb = Ridx(b);
+        double za0, za1, zb0, zb1;
+        Zc(a, za0, za1);
+        Zc(b, zb0, zb1);
+        const double q00 = Qe(J0, J0), q01 = Qe(J0, J1), q11 = Qe(J1, J1);
+        double s = Qe(Ra, Rb);
+        s += za0 * Qe(J0, Rb) + za1 * Qe(J1, Rb);
+        s += Qe(Ra, J0) * zb0 + Qe(Ra, J1) * zb1;
+        s += za0 * (q00 * zb0 + q01 * zb1) + za1 * (q01 * zb0 + q11 * zb1);
+        Ss5[lane] = s;
+    }
+    wave_lds_sync();
+    // ---- LDL^T of S, redundantly in every lane (lower triangle of S is read)
+    double L[NR][NR], dg[NR], di[NR];
+    bool pd = true;
+#pragma unroll
+    for (int j = 0; j < NR; j++) {
+        double dj = Ss5[j * NR + j];
+#pragma unroll
+        for (int k = 0; k < j; k++) dj -= L[j][k] * L[j][k] * dg[k];
+        dg[j] = dj;
+        pd = pd && (dj > 0.0);
+        di[j] = 1.0 / dj;
+#pragma unroll
+        for (int i = j + 1; i < NR; i++) {
+            double v = Ss5[i * NR + j];
+#pragma unroll
+            for (int k = 0; k < j; k++) v -= L[i][k] * L[j][k] * dg[k];
+            L[i][j] = v * di[j];
+        }
+    }
+    if (!pd) return 0;
+    // ---- right-hand side c per lane
+    auto brow = [&](int x) { return x < NJ ? x + NF : x - NJ; };  // control -> block row of Rk
+    if (lane < NRK) {
+        const int c = lane;
+        auto bu = [&](int x) {
+            if (c < NJ) return -(Hs[(NJ + x) * NV + c] + (x < NJ ? h * Ps[x * NJ + c] : 0.0));
+            return -(gsk[NJ + x] + (x < NJ ? h * ss[x] : 0.0));
+        };
+        const double bl0 = c < NJ ? -Gl[c] : -elk[0];
+        const double bl1 = c < NJ ? -Gl[NJ + c] : -elk[1];
+        const double up0 = i00 * bl0 + i01 * bl1, up1 = i10 * bl0 + i11 * bl1;
+        const double q00 = Qe(J0, J0), q01 = Qe(J0, J1), q11 = Qe(J1, J1);
+        const double bJ0 = bu(J0), bJ1 = bu(J1);
+        const double rJ0 = bJ0 - q00 * up0 - q01 * up1;
+        const double rJ1 = bJ1 - q01 * up0 - q11 * up1;
+        double y[NR], z0[NR], z1[NR], qJ0R[NR], qJ1R[NR];
+#pragma unroll
+        for (int m = 0; m < NR; m++) {
+            const int x = Ridx(m);
+            Zc(m, z0[m], z1[m]);
+            qJ0R[m] = Qe(J0, x);
+            qJ1R[m] = Qe(J1, x);
+            y[m] = bu(x) - qJ0R[m] * up0 - qJ1R[m] * up1 + z0[m] * rJ0 + z1[m] * rJ1;
+        }
+#pragma unroll
+        for (int i = 0; i < NR; i++)
+#pragma unroll
+            for (int k = 0; k < i; k++) y[i] -= L[i][k] * y[k];
+#pragma unroll
+        for (int i = 0; i < NR; i++) y[i] *= di[i];
+#pragma unroll
+        for (int i = NR - 1; i >= 0; i--)
+#pragma unroll
+            for (int k = i + 1; k < NR; k++) y[i] -= L[k][i] * y[k];
+        double uJ0 = up0, uJ1 = up1;
+#pragma unroll
+        for (int m = 0; m < NR; m++) { uJ0 += z0[m] * y[m]; uJ1 += z1[m] * y[m]; }
+        double t0 = bJ0 - q00 * uJ0 - q01 * uJ1, t1 = bJ1 - q01 * uJ0 - q11 * uJ1;
+#pragma unroll
+        for (int m = 0; m < NR; m++) { t0 -= qJ0R[m] * y[m]; t1 -= qJ1R[m] * y[m]; }
+        // D_J^T l = t  ->  l = D_J^{-T} t
+        const double l0 = i00 * t0 + i10 * t1, l1 = i01 * t0 + i11 * t1;
+#pragma unroll
+        for (int m = 0; m < NR; m++) Rk[brow(Ridx(m)) * NRK + c] = y[m];
+        Rk[brow(J0) * NRK + c] = uJ0;
+        Rk[brow(J1) * NRK + c] = uJ1;
+        Rk[NU * NRK + c] = l0;
+        Rk[(NU + 1) * NRK + c] = l1;
+    }
+    wave_lds_sync();
+    return 1;
+}
+
+}  // namespace mf
