@@ -389,7 +389,7 @@ struct MeritOut {
 
 
 template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(64) void k_ipm_iter(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+__global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
     constexpr int n = NJ, nf = NF, nl = NL;
     constexpr int NV = 2 * NJ + NF;
