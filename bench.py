@@ -3,9 +3,11 @@
 A step = one complete interior-point solve (from the initial guess to
 convergence) of this rank's shard of horizons, followed (N > 1) by the RCCL
 gather of every shard's solutions to rank 0 -- the batched configuration of
-BASELINE.json (C5: independent horizons, q0_i = q0_IK + U(-0.05, 0.05) per joint,
-line reference = fk(q0_i)[0:2]).  value = horizons that reached the KKT
-tolerance on all ranks / max-over-ranks wall time (inputs resident in HBM).
+BASELINE.json (C5: 8192 independent horizons, q0_i = q0_IK + U(-0.05, 0.05) per
+joint, line reference = fk(q0_i)[0:2]).  Every GPU solves a C5-sized batch of
+8192 horizons (weak scaling: N GPUs solve N x 8192 distinct horizons; --batch 1024
+gives C5's 8-GPU shard size).  value = horizons that reached the KKT tolerance on
+all ranks / max-over-ranks wall time (inputs resident in HBM).
 
     python bench.py [--gpus N --steps K --warmup W --batch B --nodes 100]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -59,7 +61,8 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=1024, help="horizons per GPU (C5: 8192 / 8)")
+    ap.add_argument("--batch", type=int, default=8192,
+                    help="horizons per GPU (default: the C5 batch of 8192 on every GPU, weak scaling)")
     ap.add_argument("--nodes", type=int, default=100)
     ap.add_argument("--max-iter", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")

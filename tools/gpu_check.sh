@@ -2,7 +2,7 @@
 # One GPU call: parity tests, smoke, bench (with CPU baseline), rocprof kernel stats.
 # usage: tools/gpu_check.sh TAG [BATCH]
 set -o pipefail
-TAG=${1:-run}; B=${2:-1024}
+TAG=${1:-run}; B=${2:-8192}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest.log; exit 1; }
@@ -15,3 +15,5 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python
 tail -1 $OUT/prof.log
 ls -R $OUT/prof > $OUT/prof_files.txt
 python tools/prof_summary.py "$OUT/prof/**/*.db" $OUT/rocprof_summary.md "bench.py --batch $B --steps 2 --warmup 1 ($TAG)" || true
+bash tools/pmc_traffic.sh $TAG/traffic $B > $OUT/traffic.log 2>&1 || { echo "traffic passes failed"; tail -20 $OUT/traffic.log; exit 1; }
+tail -12 $OUT/traffic.log

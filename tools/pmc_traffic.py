@@ -1,0 +1,51 @@
+"""HBM traffic per launch from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate runs,
+MI355X_MICROARCH.md HBM section), calibrated on the copy kernel of tools/traffic_run.py (known
+512 MiB read + 512 MiB written), written to profiles/pmc_traffic.json for bench.py.
+
+usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV [OUT_JSON]
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+COPY_BYTES = 64 * 1024 * 1024 * 8
+
+
+def load(fn, counter):
+    per = defaultdict(list)
+    for r in csv.DictReader(open(fn)):
+        if r["Counter_Name"] != counter:
+            continue
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        k = k.split("<")[0].replace("mf::", "")
+        per[k].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    fetch = load(sys.argv[1], "FETCH_SIZE")
+    write = load(sys.argv[2], "WRITE_SIZE")
+    out_path = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    # calibration: the largest elementwise (copy) dispatch moved exactly COPY_BYTES each way
+    cal_keys = [k for k in fetch if "elementwise" in k or "copy" in k.lower()]
+    fr = max(v for k in cal_keys for v in fetch[k])
+    wr = max(v for k in cal_keys for v in write.get(k, [0.0]))
+    f_scale, w_scale = COPY_BYTES / fr, COPY_BYTES / wr
+    res = {"calibration": {"copy_bytes_each_way": COPY_BYTES, "fetch_counter": fr, "write_counter": wr,
+                           "bytes_per_fetch_unit": f_scale, "bytes_per_write_unit": w_scale}}
+    for k in fetch:
+        if k in cal_keys or k.startswith("__amd"):
+            continue
+        fv, wv = fetch[k], write.get(k, [])
+        n = max(len(fv), 1)
+        rd = sum(fv) * f_scale / n
+        wt = sum(wv) * w_scale / max(len(wv), 1)
+        res[k] = {"launches": len(fv), "read_bytes_per_launch": rd, "write_bytes_per_launch": wt,
+                  "hbm_bytes_per_launch": rd + wt}
+    json.dump(res, open(out_path, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
