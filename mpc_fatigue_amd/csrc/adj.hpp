@@ -105,7 +105,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
         }
         matc_vec(z, A, J.axis);
         T s, cq;
-        sincos_t(in.q(i), s, cq);
+        in.sincos(i, s, cq);
         rodrigues_rows(R, A, J.axis, s, T(1.0) - cq);
         T zq[3], t[3];
         const T qdi = in.qd(i);
@@ -148,7 +148,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
         T s(0.0), omc(0.0), d[3];
         if (i > 0) {
             T cq;
-            sincos_t(in.q(i), s, cq);
+            in.sincos(i, s, cq);
             omc = T(1.0) - cq;
             // d = R_{i-1} tX = A_i uX = R_i (E_i^T uX),  E^T u = u - s (a x u) + omc (a (a.u) - u)
             const double *ax = J.axis, *u = J.uX;
@@ -346,6 +346,7 @@ template <int NJ> struct ArrIn {  // inputs from plain arrays (global memory or 
     const double *xq, *xqd;
     MF_HD double q(int i) const { return xq[i]; }
     MF_HD double qd(int i) const { return xqd[i]; }
+    MF_HD void sincos(int i, double &s, double &c) const { sincos_t(xq[i], s, c); }
 };
 
 }  // namespace mf

@@ -9,6 +9,7 @@ namespace mf {
 // Per-problem scalar state of the interior-point iteration.
 struct ProbState {
     double mu, nu, reg_last, E0, cviol, obj;
+    double tau_fb, pcorr;  // fraction to the boundary, step-curvature correction (k_ipm_kkt -> k_ipm_post)
     int reg_tier;     // inertia correction of the last iteration: 0 none, 1 force block, 2 all primal
     int status;       // -1 running, 0 converged, 1 max_iter, 2 line-search failure, 3 inertia failure
     int iter, n_ls_fail, n_ic, consec_fail;

@@ -121,9 +121,15 @@ template <int NJ> struct ModelLds {
 // (what the Riccati recursion needs at delta_w = delta_c = 0).
 template <int NJ, int NF> struct NodeIn {
     const double *xq, *xqd;
+    const double (*sc)[2];  // LDS: sin / cos of the node's joint angles (one evaluation per node, not per lane)
     int v;
     __device__ __forceinline__ Dual q(int i) const { return Dual(xq[i], v == i ? 1.0 : 0.0); }
     __device__ __forceinline__ Dual qd(int i) const { return Dual(xqd[i], v == NJ + i ? 1.0 : 0.0); }
+    __device__ __forceinline__ void sincos(int i, Dual &s, Dual &c) const {
+        const double sv = sc[i][0], cv = sc[i][1], t = (v == i) ? 1.0 : 0.0;
+        s = Dual(sv, cv * t);
+        c = Dual(cv, -sv * t);
+    }
 };
 template <int NJ, int NF, int NPB, int NV> struct NodeOut {
     double (*Js)[NJ][NV];  // LDS: Jacobian columns of the block's nodes
@@ -159,6 +165,7 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
     __shared__ double Js[NPB][NJ][NV], Hs[NPB][NV][NV], Ts[NPB][NJ], Cs[NPB][NJ];
+    __shared__ double SCs[NPB][NJ][2];  // sin / cos of each node's joint angles
     Ml.load(Mg);
     stage_lds(&F, Fg);
     const int tid = threadIdx.x, g = tid / NV, v = tid % NV;
@@ -182,6 +189,7 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     out.g = g;
     out.v = v;
     out.fdir = C.fdir;
+    if (run && v < NJ) sincos(q[v], &SCs[g][v][0], &SCs[g][v][1]);
     // torque weights c = y_tau + 2 wtau tau (tau at the iterate first when wtau != 0)
     if (run && v == 0) {
         const double *yd = A.yd + b * S.u + (size_t)k * NJ;
@@ -223,7 +231,7 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
             Fw[r] = acc;
         }
         const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
-        NodeIn<NJ, NF> in{q, qd, v};
+        NodeIn<NJ, NF> in{q, qd, SCs[g], v};
         node_fwd_rev<Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
     }
     __syncthreads();
@@ -369,6 +377,7 @@ struct TrialIn {
     double al;
     __device__ double q(int i) const { return xq[i] + al * dxq[i]; }
     __device__ double qd(int i) const { return xqd[i] + al * dxqd[i]; }
+    __device__ void sincos(int i, double &s, double &c) const { sincos_t(q(i), s, c); }
 };
 // accumulates wtau |tau|^2, |tau - s| on the bounded torque rows and |p - ref| on the line
 struct MeritOut {
@@ -389,7 +398,13 @@ struct MeritOut {
 
 
 template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+// One interior-point iteration = k_eval_node + three per-problem launches (one wave per
+// problem each; a launch boundary lets each phase have its own register budget):
+//   k_ipm_pre  : optimality error, convergence test, barrier update, barrier Sigma / gradients
+//   k_ipm_kkt  : inertia-corrected Riccati recursion, forward sweep, step recovery
+//   k_ipm_post : fraction to the boundary, merit line search, update
+// Scalars that cross a boundary travel in ProbState (mu, nu, tau_fb, pcorr, regularisation).
+__global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
     constexpr int n = NJ, nf = NF, nl = NL;
     constexpr int NV = 2 * NJ + NF;
@@ -440,13 +455,26 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
     const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
     double mu = st.mu, nu = st.nu;
-
+    constexpr int UB = 4;  // element-loop chunk (see the optimality-error phase)
+    auto finish = [&](int status) {
+        STAMP_FLUSH;
+        double f = 0.0;
+        for (int k = lane; k < N; k += 64) f += cost[k];
+        f = wave_sum(f);
+        if (lane == 0) {
+            st.status = status;
+            st.obj = f;
+            st.mu = mu;
+            st.nu = nu;
+            A.st[b] = st;
+            atomicSub(A.active, 1);
+        }
+    };
     // ---------------- optimality error
     // Element loops of one problem run in chunks of UB elements per lane.  A chunk issues every
     // load first (indices clamped into range, results past the end discarded) and only then
     // computes and stores, so it costs one global-memory round trip instead of one per element:
     // one wave per problem has no other waves of its own to hide that latency behind.
-    constexpr int UB = 4;
     double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sum_mult = 0, sum_bmult = 0;
     int n_mult = 0, n_bmult = 0;
     auto comp = [&](double z, double gap) {
@@ -570,20 +598,6 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
     double Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
     st.E0 = E0;
     st.cviol = pinf;
-    auto finish = [&](int status) {
-        STAMP_FLUSH;
-        double f = 0.0;
-        for (int k = lane; k < N; k += 64) f += cost[k];
-        f = wave_sum(f);
-        if (lane == 0) {
-            st.status = status;
-            st.obj = f;
-            st.mu = mu;
-            st.nu = nu;
-            A.st[b] = st;
-            atomicSub(A.active, 1);
-        }
-    };
     if (E0 <= C.tol && pinf <= C.constr_viol_tol) { finish(ST_CONVERGED); return; }
     if (st.iter >= C.max_iter) { finish(ST_MAXITER); return; }
     while (Emu <= kappa_eps * mu && mu > C.tol / 10.0) {
@@ -672,6 +686,83 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
     __syncthreads();
 
     STAMP(1);
+    STAMP_FLUSH;
+    if (lane == 0) {
+        st.mu = mu;
+        st.nu = nu;
+        st.tau_fb = tau_fb;
+        A.st[b] = st;
+    }
+#undef TACT
+}
+
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                                 OcpConst C, IpmArrays A, int batch) {
+    constexpr int n = NJ, nf = NF, nl = NL;
+    constexpr int NV = 2 * NJ + NF;
+    constexpr int NFA = NF > 0 ? NF : 1;
+    constexpr int NLA = NL > 0 ? NL : 1;
+    constexpr int MB = 3 * NJ + NF + NL;
+    __shared__ ModelLds<NJ> Ml;
+    const DevModel &M = Ml.get();
+    __shared__ DevFrame F;
+    __shared__ int perm[MB], piv[MB];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b >= batch) return;
+    ProbState st = A.st[b];
+    if (st.status != ST_RUNNING) return;
+    Ml.load(Mg);
+    stage_lds(&F, Fg);
+    __shared__ double Bnd[4 * NJ];  // q_lo, q_hi, qd_lo, qd_hi (kernel-argument arrays read per element)
+    if (lane < NJ) {
+        Bnd[lane] = C.q_lo[lane];
+        Bnd[NJ + lane] = C.q_hi[lane];
+        Bnd[2 * NJ + lane] = C.qd_lo[lane];
+        Bnd[3 * NJ + lane] = C.qd_hi[lane];
+    }
+    __syncthreads();
+    STAMP_INIT;
+
+    const IpmSizes S = ipm_sizes(C);
+    const int N = C.N;
+    const double h = C.h;
+    double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *Fv = A.F + b * S.f, *s = A.s + b * S.u;
+    double *yc = A.yc + b * S.u, *yl = A.yl + b * S.l, *yd = A.yd + b * S.u;
+    double *zqL = A.zqL + b * S.q, *zqU = A.zqU + b * S.q, *zdL = A.zdL + b * S.u, *zdU = A.zdU + b * S.u;
+    double *vL = A.vL + b * S.u, *vU = A.vU + b * S.u;
+    double *dq = A.dq + b * S.q, *dqd = A.dqd + b * S.u, *dF = A.dF + b * S.f, *ds = A.ds + b * S.u;
+    double *dyc = A.dyc + b * S.u, *dyl = A.dyl + b * S.l, *dyd = A.dyd + b * S.u;
+    double *dzqL = A.dzqL + b * S.q, *dzqU = A.dzqU + b * S.q, *dzdL = A.dzdL + b * S.u, *dzdU = A.dzdU + b * S.u;
+    double *dvL = A.dvL + b * S.u, *dvU = A.dvU + b * S.u;
+    const double *tau = A.tau + b * S.u, *Jt = A.Jt + b * S.jt, *line = A.line + b * S.l, *Jl = A.Jl + b * S.jl;
+    const double *W = A.W + b * S.w, *gf = A.gf + b * S.gf, *cost = A.cost + b * S.cost;
+    double *Sxq = A.Sxq + b * S.q, *gphq = A.gphq + b * S.q, *Sxd = A.Sxd + b * S.u, *gphd = A.gphd + b * S.u;
+    double *Ss = A.Ss + b * S.u, *gphs = A.gphs + b * S.u;
+    double *G = A.G + b * S.G, *wv = A.wv + b * S.wv;
+    const double *lref = A.lref + b * 2;
+    const double *tlo = A.tau_lo, *thi = A.tau_hi;
+    const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
+#define TACT(k, j) (hasb(tlo[(k) * n + (j)]) || hasb(thi[(k) * n + (j)]))
+
+    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
+    const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
+    double mu = st.mu, nu = st.nu;
+    constexpr int UB = 2;  // element-loop chunk (see the optimality-error phase)
+    auto finish = [&](int status) {
+        STAMP_FLUSH;
+        double f = 0.0;
+        for (int k = lane; k < N; k += 64) f += cost[k];
+        f = wave_sum(f);
+        if (lane == 0) {
+            st.status = status;
+            st.obj = f;
+            st.mu = mu;
+            st.nu = nu;
+            A.st[b] = st;
+            atomicSub(A.active, 1);
+        }
+    };
     // ---------------- inertia-corrected Riccati recursion
     // Stage k (1 <= k < N): x = dq_k (n), u = (dqd_k, dF_k) (NU), dynamics dx_{k+1} = dx_k + B du_k + c_k
     // with B = [h I, 0].  The line constraint of stage k+1 is pushed back onto stage k:
@@ -1183,6 +1274,83 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
     __syncthreads();
 
     STAMP(3);
+    pcorr = wave_sum(pcorr);
+    STAMP_FLUSH;
+    if (lane == 0) {
+        st.pcorr = pcorr;
+        A.st[b] = st;
+    }
+#undef TACT
+}
+
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                                 OcpConst C, IpmArrays A, int batch) {
+    constexpr int n = NJ, nf = NF, nl = NL;
+    constexpr int NV = 2 * NJ + NF;
+    constexpr int NFA = NF > 0 ? NF : 1;
+    constexpr int NLA = NL > 0 ? NL : 1;
+    constexpr int MB = 3 * NJ + NF + NL;
+    __shared__ ModelLds<NJ> Ml;
+    const DevModel &M = Ml.get();
+    __shared__ DevFrame F;
+    __shared__ int perm[MB], piv[MB];
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b >= batch) return;
+    ProbState st = A.st[b];
+    if (st.status != ST_RUNNING) return;
+    Ml.load(Mg);
+    stage_lds(&F, Fg);
+    __shared__ double Bnd[4 * NJ];  // q_lo, q_hi, qd_lo, qd_hi (kernel-argument arrays read per element)
+    if (lane < NJ) {
+        Bnd[lane] = C.q_lo[lane];
+        Bnd[NJ + lane] = C.q_hi[lane];
+        Bnd[2 * NJ + lane] = C.qd_lo[lane];
+        Bnd[3 * NJ + lane] = C.qd_hi[lane];
+    }
+    __syncthreads();
+    STAMP_INIT;
+
+    const IpmSizes S = ipm_sizes(C);
+    const int N = C.N;
+    const double h = C.h;
+    double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *Fv = A.F + b * S.f, *s = A.s + b * S.u;
+    double *yc = A.yc + b * S.u, *yl = A.yl + b * S.l, *yd = A.yd + b * S.u;
+    double *zqL = A.zqL + b * S.q, *zqU = A.zqU + b * S.q, *zdL = A.zdL + b * S.u, *zdU = A.zdU + b * S.u;
+    double *vL = A.vL + b * S.u, *vU = A.vU + b * S.u;
+    double *dq = A.dq + b * S.q, *dqd = A.dqd + b * S.u, *dF = A.dF + b * S.f, *ds = A.ds + b * S.u;
+    double *dyc = A.dyc + b * S.u, *dyl = A.dyl + b * S.l, *dyd = A.dyd + b * S.u;
+    double *dzqL = A.dzqL + b * S.q, *dzqU = A.dzqU + b * S.q, *dzdL = A.dzdL + b * S.u, *dzdU = A.dzdU + b * S.u;
+    double *dvL = A.dvL + b * S.u, *dvU = A.dvU + b * S.u;
+    const double *tau = A.tau + b * S.u, *Jt = A.Jt + b * S.jt, *line = A.line + b * S.l, *Jl = A.Jl + b * S.jl;
+    const double *W = A.W + b * S.w, *gf = A.gf + b * S.gf, *cost = A.cost + b * S.cost;
+    double *Sxq = A.Sxq + b * S.q, *gphq = A.gphq + b * S.q, *Sxd = A.Sxd + b * S.u, *gphd = A.gphd + b * S.u;
+    double *Ss = A.Ss + b * S.u, *gphs = A.gphs + b * S.u;
+    double *G = A.G + b * S.G, *wv = A.wv + b * S.wv;
+    const double *lref = A.lref + b * 2;
+    const double *tlo = A.tau_lo, *thi = A.tau_hi;
+    const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
+#define TACT(k, j) (hasb(tlo[(k) * n + (j)]) || hasb(thi[(k) * n + (j)]))
+
+    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
+    const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
+    double mu = st.mu, nu = st.nu;
+    constexpr int UB = 2;  // element-loop chunk (see the optimality-error phase)
+    auto finish = [&](int status) {
+        STAMP_FLUSH;
+        double f = 0.0;
+        for (int k = lane; k < N; k += 64) f += cost[k];
+        f = wave_sum(f);
+        if (lane == 0) {
+            st.status = status;
+            st.obj = f;
+            st.mu = mu;
+            st.nu = nu;
+            A.st[b] = st;
+            atomicSub(A.active, 1);
+        }
+    };
+    const double tau_fb = st.tau_fb;
     // ---------------- fraction to boundary
     double ap = 1.0, az = 1.0;
     auto ftbL = [&](double x, double dx, double lo, double &a) { if (dx < 0) a = fmin(a, -tau_fb * (x - lo) / dx); };
@@ -1239,15 +1407,13 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
         double f = 0, bar = 0, th = 0;
         int bad = 0;
         for (int k = lane; k < N; k += 64) {
-            double tq[NJ], tqd[NJ], qn[NJ], sl[NJ], lo[NJ], hi[NJ], Fw[3], c = 0.0;
+            // only the sweep's inputs are held through the sweep; slacks, bounds and q_{k+1} are
+            // read after it (register budget of the sweep)
+            double tq[NJ], tqd[NJ], tv[NJ], Fw[3], c = 0.0;
 #pragma unroll
             for (int j = 0; j < NJ; j++) {
                 tq[j] = q[k * n + j] + alpha * dq[k * n + j];
                 tqd[j] = qd[k * n + j] + alpha * dqd[k * n + j];
-                qn[j] = q[(k + 1) * n + j] + alpha * dq[(k + 1) * n + j];
-                sl[j] = s[k * n + j] + alpha * ds[k * n + j];
-                lo[j] = tlo[k * n + j];
-                hi[j] = thi[k * n + j];
             }
 #pragma unroll
             for (int r = 0; r < 3; r++) Fw[r] = 0.0;
@@ -1259,8 +1425,9 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
                 for (int r = 0; r < 3; r++) Fw[r] += tF * C.fdir[3 * a + r];
             }
             struct MOut {
-                const double *sl, *lo, *hi, *lref;
-                double wtau, c, th;
+                double *tv;
+                const double *lref;
+                double th;
                 int nl;
                 bool line;
                 __device__ void frame(const double *p) {
@@ -1268,19 +1435,20 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
                         for (int l = 0; l < nl; l++) th += fabs(p[l] - lref[l]);
                 }
                 __device__ void force(const double *) {}
-                __device__ void joint(int j, double t, double, double) {
-                    c += wtau * t * t;
-                    if (hasb(lo[j]) || hasb(hi[j])) th += fabs(t - sl[j]);
-                }
-            } mo{sl, lo, hi, lref, C.wtau, 0.0, 0.0, nl, LINE_ON(k)};
+                __device__ void joint(int j, double t, double, double) { tv[j] = t; }
+            } mo{tv, lref, 0.0, nl, LINE_ON(k)};
             ArrIn<NJ> tin{tq, tqd};
             node_values<NJ>(M, F, fpj, tin, Fw, mo);
 #pragma unroll
             for (int j = 0; j < NJ; j++) {
-                c += C.wqd * tqd[j] * tqd[j];
-                th += fabs(tq[j] + h * tqd[j] - qn[j]);
+                const double sl = s[k * n + j] + alpha * ds[k * n + j];
+                const double qn = q[(k + 1) * n + j] + alpha * dq[(k + 1) * n + j];
+                const double lo = tlo[k * n + j], hi = thi[k * n + j];
+                c += C.wqd * tqd[j] * tqd[j] + C.wtau * tv[j] * tv[j];
+                if (hasb(lo) || hasb(hi)) th += fabs(tv[j] - sl);
+                th += fabs(tq[j] + h * tqd[j] - qn);
             }
-            f += c + mo.c;
+            f += c;
             th += mo.th;
         }
         for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
@@ -1324,7 +1492,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
         merit(0.0, phi0, th0, ok0);
     }
     // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx; lane e covers row v of node k's W
-    double gdot = 0, pHp = pcorr;
+    double gdot = 0, pHp = (lane == 0) ? st.pcorr : 0.0;  // pcorr: whole-wave sum from k_ipm_kkt
     for (int e0 = lane; e0 < N * NV; e0 += 64 * 2) {
         double acc[2], gd[2];
 #pragma unroll
@@ -1470,6 +1638,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_iter(const DevModel *__restrict__
 #undef TACT
 }
 
+
 // ============================================================== output in the reference layout
 template <int NJ, int NF>
 __global__ __launch_bounds__(64) void k_ipm_output(OcpConst C, IpmArrays A, int batch, double *w, int *status,
@@ -1509,7 +1678,7 @@ struct IpmLaunch {
                      hipStream_t s) {
         hipLaunchKernelGGL((k_ipm_init<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
     }
-    // phase 0: node derivatives (k_eval_node), 1: per-problem IPM step (k_ipm_iter)
+    // phase 0: node derivatives (k_eval_node), 1..3: per-problem IPM phases (k_ipm_pre, k_ipm_kkt, k_ipm_post)
     static void iter(int phase, const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A,
                      int batch, hipStream_t s) {
         constexpr int NV = 2 * NJ + NF;
@@ -1519,7 +1688,9 @@ struct IpmLaunch {
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3((unsigned)((nodes + NPB - 1) / NPB)), dim3(256), 0, s,
                                M, F, C, A, batch);
         else {
-            hipLaunchKernelGGL((k_ipm_iter<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+            if (phase == 1) hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+            else if (phase == 2) hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+            else hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
         }
     }
     static void output(const OcpConst &C, const IpmArrays &A, int batch, double *w, int *status, int *iters,
@@ -1540,7 +1711,7 @@ bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevF
 #define MF_CASE(NJ, NF, NL)                                                       \
     if (n == NJ && nf == NF && nl == NL) {                                        \
         if (what == 0) IpmLaunch<NJ, NF, NL>::init(M, F, C, A, batch, s);          \
-        else if (what >= 10 && what <= 11) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
+        else if (what >= 10 && what <= 13) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
         else IpmLaunch<NJ, NF, NL>::output(C, A, batch, w, status, iters, kkt, obj, s); \
         return true;                                                              \
     }
