@@ -112,10 +112,13 @@ template <int NJ> struct ModelLds {
 };
 
 // ============================================================== eval: node derivatives
-// Lanes (problem, node, direction v), NV = 2 n + n_f lanes per node, NPB nodes per
-// block.  Each lane runs node_fwd_rev<Dual> (adj.hpp) with tangent e_v and gets tau,
-// column v of d tau / dw, the line Jacobian column and column v of the exact Hessian
-// of phi = c.tau + yl.line, c = y_tau + 2 wtau tau.  The block exchanges the Jacobian
+// Lanes (problem, node, direction v), NVL = 2 n lanes per node (the q and qd directions),
+// NPB nodes per block.  Each lane runs node_fwd_rev<Dual> (adj.hpp) with tangent e_v and
+// gets tau, column v of d tau / dw, the line Jacobian column and column v of the exact
+// Hessian of phi = c.tau + yl.line, c = y_tau + 2 wtau tau.  The force directions need no
+// lane of their own: phi is linear in F, so the force row of the Hessian comes out of the
+// q / qd lanes (symmetry), H_FF = 0, and d tau / dF_a = -J_f^T fdir_a = -(fdir_a . dp_f/dq_j)
+// is the frame-point tangent of the q lanes.  The block exchanges the Jacobian
 // columns through LDS to add the Gauss-Newton / barrier term and writes the condensed
 // stage Hessian  H0_k = grad^2 L_k + J^T diag(2 wtau + Sigma_s) J + diag(Sigma_x)
 // (what the Riccati recursion needs at delta_w = delta_c = 0).
@@ -159,8 +162,9 @@ template <int NJ, int NF, int NL>
 __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                    OcpConst C, IpmArrays A, int batch) {
     constexpr int NV = 2 * NJ + NF;
+    constexpr int NVL = 2 * NJ;
     constexpr int NFA = NF > 0 ? NF : 1;
-    constexpr int NPB = 256 / NV;
+    constexpr int NPB = 256 / NVL;
     __shared__ ModelLds<NJ> Ml;
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     __shared__ double SCs[NPB][NJ][2];  // sin / cos of each node's joint angles
     Ml.load(Mg);
     stage_lds(&F, Fg);
-    const int tid = threadIdx.x, g = tid / NV, v = tid % NV;
+    const int tid = threadIdx.x, g = tid / NVL, v = tid % NVL;
     const int N = C.N;
     const long node = (long)blockIdx.x * NPB + g;
     bool run = (g < NPB) && node < (long)batch * N;
@@ -233,6 +237,17 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
         const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
         NodeIn<NJ, NF> in{q, qd, SCs[g], v};
         node_fwd_rev<Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
+        // force columns: d tau_v / dF_a = -fdir_a . dp_f/dq_v (q lanes), H_FF = 0
+        if (v < NJ)
+#pragma unroll
+            for (int a = 0; a < NF; a++)
+                Js[g][v][2 * NJ + a] = -(C.fdir[3 * a] * out.pfd[0] + C.fdir[3 * a + 1] * out.pfd[1] +
+                                         C.fdir[3 * a + 2] * out.pfd[2]);
+        if (v == 0)
+#pragma unroll
+            for (int a = 0; a < NF; a++)
+#pragma unroll
+                for (int c2 = 0; c2 < NF; c2++) Hs[g][2 * NJ + a][2 * NJ + c2] = 0.0;
     }
     __syncthreads();
     if (!run) return;
@@ -254,19 +269,25 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
         }
     }
     if (v >= NJ && v < 2 * NJ) diag += 2.0 * C.wqd;
-    if (v >= 2 * NJ) diag += 2.0 * C.wF;
     double *W = A.W + b * S.w + (size_t)k * NV * NV;
-#pragma unroll
-    for (int u = 0; u < NV; u++) {
-        if (u < v) continue;
+    // entry (u, c) = (c, u) of H0, u >= c
+    auto went = [&](int u, int c, double dg) {
         double gn = 0.0;
 #pragma unroll
-        for (int j = 0; j < NJ; j++) gn += wj[j] * Js[g][j][u] * Js[g][j][v];
-        double hh = Hs[g][u][v] + gn;
-        if (u == v) hh += diag;
-        W[u * NV + v] = hh;
-        W[v * NV + u] = hh;
-    }
+        for (int j = 0; j < NJ; j++) gn += wj[j] * Js[g][j][u] * Js[g][j][c];
+        double hh = Hs[g][u][c] + gn;
+        if (u == c) hh += dg;
+        W[u * NV + c] = hh;
+        W[c * NV + u] = hh;
+    };
+#pragma unroll
+    for (int u = 0; u < NV; u++)
+        if (u >= v) went(u, v, diag);
+    if (v == 0)  // force-force block (no lane of its own)
+#pragma unroll
+        for (int a = 0; a < NF; a++)
+#pragma unroll
+            for (int c2 = 0; c2 <= a; c2++) went(2 * NJ + a, 2 * NJ + c2, 2.0 * C.wF);
     double *Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
     double gfv = 0.0;
 #pragma unroll
@@ -276,8 +297,18 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
         gfv += 2.0 * C.wtau * Ts[g][j] * jv;
     }
     if (v >= NJ && v < 2 * NJ) gfv += 2.0 * C.wqd * qd[v - NJ];
-    if (NF > 0 && v >= 2 * NJ) gfv += 2.0 * C.wF * Fv[v - 2 * NJ];
     A.gf[b * S.gf + (size_t)k * NV + v] = gfv;
+    if (v < NJ)
+#pragma unroll
+        for (int a = 0; a < NF; a++) Jt[v * NV + 2 * NJ + a] = Js[g][v][2 * NJ + a];
+    if (v == 0)
+#pragma unroll
+        for (int a = 0; a < NF; a++) {
+            double ga = 2.0 * C.wF * Fv[a];
+#pragma unroll
+            for (int j = 0; j < NJ; j++) ga += 2.0 * C.wtau * Ts[g][j] * Js[g][j][2 * NJ + a];
+            A.gf[b * S.gf + (size_t)k * NV + 2 * NJ + a] = ga;
+        }
     if (NL > 0 && v < NJ) {
         double *Jl = A.Jl + b * S.jl + (size_t)k * NL * NJ;
 #pragma unroll
@@ -1681,8 +1712,7 @@ struct IpmLaunch {
     // phase 0: node derivatives (k_eval_node), 1..3: per-problem IPM phases (k_ipm_pre, k_ipm_kkt, k_ipm_post)
     static void iter(int phase, const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A,
                      int batch, hipStream_t s) {
-        constexpr int NV = 2 * NJ + NF;
-        constexpr int NPB = 256 / NV;
+        constexpr int NPB = 256 / (2 * NJ);  // k_eval_node: 2 NJ lanes per node
         long nodes = (long)batch * C.N;
         if (phase == 0)
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3((unsigned)((nodes + NPB - 1) / NPB)), dim3(256), 0, s,
