@@ -36,8 +36,8 @@
 namespace mf {
 
 // world inertia (about the com) applied to v: R Ic R^T v
-template <class T> MF_HD void inertia_apply(T *o, const T *R, const double *Ic, const T *v) {
-    T l[3], t[3];
+template <class TO, class TR, class TV> MF_HD void inertia_apply(TO *o, const TR *R, const double *Ic, const TV *v) {
+    TO l[3], t[3];
     matT_vec(l, R, v);
     cmat_vec(t, Ic, l);
     mat_vec(o, R, t);
@@ -60,8 +60,15 @@ template <class T> MF_HD void rodrigues_rows(T *R, const T *A, const double *ax,
     }
 }
 
+// Two scalar types: TP for the pose quantities (functions of q only: rotations, joint origins
+// and axes, com and frame points, the c-weighted axis prefix sums) and TV for everything that
+// also depends on qd (twists, accelerations, wrenches, torques, all adjoints).  A lane whose
+// tangent direction is a joint velocity runs TP = double, TV = Dual: the pose tangent is
+// identically zero there, and its arithmetic drops to plain FP64.  TP = TV = Dual for the q
+// directions, TP = TV = double for values only.
 // fp: frame parent joint (-1: no frame point / external force).
-// in.q(i), in.qd(i): inputs as T.  Fw: world force applied at p_f (zeros without force).
+// in.q(i), in.sincos(i, s, c) as TP, in.qd(i) as TV.  Fw: world force applied at p_f (zeros
+// without force; a constant: the force column of the derivatives needs no tangent, k_eval_node).
 // c: torque weights (NJ; indexed by the running joint, so keep it in memory, not registers),
 // yl: frame-point weights (3, zero padded).  The joint loops are deliberately not
 // unrolled: one iteration's working set fits in registers, six interleaved do not.
@@ -69,32 +76,34 @@ template <class T> MF_HD void rodrigues_rows(T *R, const T *A, const double *ax,
 // em.joint(i, tau_i, dphi/dq_i, dphi/dqd_i) during the reverse sweep (i = NJ-1 .. 0).
 // ADJ = false: values only (tau, p_f), the same arithmetic without the adjoint
 // statements (used by the line search and the initial slacks).
-template <class T, int NJ, bool ADJ = true, class In, class Emit>
-MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &in, const T *Fw, const double *c,
+template <class TP, class TV, int NJ, bool ADJ = true, class In, class Emit>
+MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &in, const double *Fw, const double *c,
                         const double *yl, Emit &em) {
-    T R[9], o[3], w[3], dw[3], a[3], Lz[3], Loz[3];
+    TP R[9], o[3], Lz[3], Loz[3];
+    TV w[3], dw[3], a[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        w[k] = T(0.0); dw[k] = T(0.0); a[k] = T(-M.g[k]);
-        Lz[k] = T(0.0); Loz[k] = T(0.0);
+        w[k] = TV(0.0); dw[k] = TV(0.0); a[k] = TV(-M.g[k]);
+        Lz[k] = TP(0.0); Loz[k] = TP(0.0);
     }
 
     // ---------------- forward sweep: pose, twist, acceleration; prefix Lambda
 #pragma unroll 1
     for (int i = 0; i < NJ; i++) {
         const DevJoint &J = M.j[i];
-        T A[9], on[3], z[3];
+        TP A[9], on[3], z[3];
         if (i == 0) {
 #pragma unroll
-            for (int k = 0; k < 9; k++) A[k] = T(J.RX[k]);
+            for (int k = 0; k < 9; k++) A[k] = TP(J.RX[k]);
 #pragma unroll
-            for (int k = 0; k < 3; k++) on[k] = T(J.tX[k]);
+            for (int k = 0; k < 3; k++) on[k] = TP(J.tX[k]);
         } else {
             matc_mul(A, R, J.RX);
             matc_vec(on, R, J.tX);
 #pragma unroll
             for (int k = 0; k < 3; k++) on[k] = on[k] + o[k];
-            T d[3], t1[3], t2[3];
+            TP d[3];
+            TV t1[3], t2[3];
 #pragma unroll
             for (int k = 0; k < 3; k++) d[k] = on[k] - o[k];
             cross3(t1, dw, d);
@@ -104,18 +113,18 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
             for (int k = 0; k < 3; k++) a[k] = a[k] + t1[k] + t2[k];
         }
         matc_vec(z, A, J.axis);
-        T s, cq;
+        TP s, cq;
         in.sincos(i, s, cq);
-        rodrigues_rows(R, A, J.axis, s, T(1.0) - cq);
-        T zq[3], t[3];
-        const T qdi = in.qd(i);
+        rodrigues_rows(R, A, J.axis, s, TP(1.0) - cq);
+        TV zq[3], t[3];
+        const TV qdi = in.qd(i);
 #pragma unroll
         for (int k = 0; k < 3; k++) zq[k] = z[k] * qdi;
         cross3(t, w, zq);
 #pragma unroll
         for (int k = 0; k < 3; k++) { dw[k] = dw[k] + t[k]; w[k] = w[k] + zq[k]; o[k] = on[k]; }
         if constexpr (ADJ) {
-            T oz[3];
+            TP oz[3];
             cross3(oz, o, z);
 #pragma unroll
             for (int k = 0; k < 3; k++) { Lz[k] += z[k] * c[i]; Loz[k] += oz[k] * c[i]; }
@@ -123,91 +132,92 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
     }
 
     // ---------------- reverse sweep
-    T Mt[3], Ft[3], wb[3], dwb[3], ab[3], G[3], Ob[3];
+    TV Mt[3], Ft[3], wb[3], dwb[3], ab[3], G[3], Ob[3];
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        Mt[k] = T(0.0); Ft[k] = T(0.0); wb[k] = T(0.0); dwb[k] = T(0.0);
-        ab[k] = T(0.0); G[k] = T(0.0); Ob[k] = T(0.0);
+        Mt[k] = TV(0.0); Ft[k] = TV(0.0); wb[k] = TV(0.0); dwb[k] = TV(0.0);
+        ab[k] = TV(0.0); G[k] = TV(0.0); Ob[k] = TV(0.0);
     }
 #pragma unroll 1
     for (int i = NJ - 1; i >= 0; i--) {
         const DevJoint &J = M.j[i];
         const double m = J.m;
-        const T qdi = in.qd(i);
-        T z[3];
+        const TV qdi = in.qd(i);
+        TP z[3];
         matc_vec(z, R, J.axis);  // z_i = A_i axis = R_i axis (E_i leaves the axis fixed)
-        T zq[3], wp[3], dwp[3];
+        TV zq[3], wp[3], dwp[3];
         {
-            T t[3];
+            TV t[3];
 #pragma unroll
             for (int k = 0; k < 3; k++) { zq[k] = z[k] * qdi; wp[k] = w[k] - zq[k]; }
             cross3(t, wp, zq);
 #pragma unroll
             for (int k = 0; k < 3; k++) dwp[k] = dw[k] - t[k];
         }
-        T s(0.0), omc(0.0), d[3];
+        TP s(0.0), omc(0.0), d[3];
         if (i > 0) {
-            T cq;
+            TP cq;
             in.sincos(i, s, cq);
-            omc = T(1.0) - cq;
+            omc = TP(1.0) - cq;
             // d = R_{i-1} tX = A_i uX = R_i (E_i^T uX),  E^T u = u - s (a x u) + omc (a (a.u) - u)
             const double *ax = J.axis, *u = J.uX;
             const double axu0 = ax[1] * u[2] - ax[2] * u[1], axu1 = ax[2] * u[0] - ax[0] * u[2],
                          axu2 = ax[0] * u[1] - ax[1] * u[0];
             const double au = ax[0] * u[0] + ax[1] * u[1] + ax[2] * u[2];
-            T eu[3];
-            eu[0] = T(u[0]) - s * axu0 + omc * (au * ax[0] - u[0]);
-            eu[1] = T(u[1]) - s * axu1 + omc * (au * ax[1] - u[1]);
-            eu[2] = T(u[2]) - s * axu2 + omc * (au * ax[2] - u[2]);
+            TP eu[3];
+            eu[0] = TP(u[0]) - s * axu0 + omc * (au * ax[0] - u[0]);
+            eu[1] = TP(u[1]) - s * axu1 + omc * (au * ax[1] - u[1]);
+            eu[2] = TP(u[2]) - s * axu2 + omc * (au * ax[2] - u[2]);
             mat_vec(d, R, eu);
         }
         // link wrench about the world origin
-        T r[3], cw[3], f[3];
+        TP r[3], cw[3];
+        TV f[3];
         matc_vec(r, R, J.c);
         {
-            T t1[3], t2[3];
+            TV t1[3], t2[3];
             cross3(t1, dw, r);
             cross3(t2, w, r);
             cross3(t2, w, t2);
 #pragma unroll
             for (int k = 0; k < 3; k++) { cw[k] = o[k] + r[k]; f[k] = (a[k] + t1[k] + t2[k]) * m; }
         }
-        T v1[3], v2[3];
+        TV v1[3], v2[3];
         inertia_apply(v1, R, J.Ic, dw);
         inertia_apply(v2, R, J.Ic, w);
         {
-            T t1[3], t2[3];
+            TV t1[3], t2[3];
             cross3(t1, cw, f);
             cross3(t2, w, v2);
 #pragma unroll
             for (int k = 0; k < 3; k++) { Mt[k] += t1[k] + v1[k] + t2[k]; Ft[k] += f[k]; }
         }
-        T pf[3];
+        TP pf[3];
         if (i == fp) {
             frame_point(F, o, R, pf);
             em.frame(pf);
-            T pxF[3];
+            TP pxF[3];
             cross3(pxF, pf, Fw);
 #pragma unroll
             for (int k = 0; k < 3; k++) { Mt[k] = Mt[k] - pxF[k]; Ft[k] = Ft[k] - Fw[k]; }
         }
-        T oz[3];
+        TP oz[3];
         cross3(oz, o, z);
-        const T taui = dot3(z, Mt) + dot3(oz, Ft);
+        const TV taui = dot3(z, Mt) + dot3(oz, Ft);
 
-        T gqi(0.0), gqdi(0.0), db[3];  // db: adjoint of d_i = o_i - o_{i-1}; o_{i-1} receives -db
+        TV gqi(0.0), gqdi(0.0), db[3];  // db: adjoint of d_i = o_i - o_{i-1}; o_{i-1} receives -db
         if constexpr (ADJ) {
         // ---- adjoints of link i's quantities (M_bar = Lz, f_bar = Loz)
-        T zb[3], ob[3], cwb[3];
+        TV zb[3], ob[3], cwb[3];
         {
-            T FxO[3], ZxF[3];
+            TV FxO[3], ZxF[3];
             cross3(FxO, Ft, o);
             cross3(ZxF, z, Ft);
 #pragma unroll
             for (int k = 0; k < 3; k++) { zb[k] = (Mt[k] + FxO[k]) * c[i]; ob[k] = ZxF[k] * c[i]; }
         }
         if (i == fp) {
-            T pfb[3], g1[3], t1[3];
+            TP pfb[3], g1[3], t1[3];
             cross3(pfb, Lz, Fw);
 #pragma unroll
             for (int k = 0; k < 3; k++) pfb[k] = pfb[k] + yl[k];
@@ -220,29 +230,30 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
             for (int k = 0; k < 3; k++) { G[k] += t1[k]; Ob[k] += pfb[k]; }
         }
         cross3(cwb, f, Lz);
-        T ft[3];
+        TP ft[3];
         {
-            T t1[3];
+            TP t1[3];
             cross3(t1, Lz, cw);
 #pragma unroll
             for (int k = 0; k < 3; k++) ft[k] = Loz[k] + t1[k];
         }
         {
-            T u1[3], mw[3], u2[3];
+            TP u1[3], rxf[3];
+            TV mw[3], u2[3], vxl[3];
             inertia_apply(u1, R, J.Ic, Lz);
             cross3(mw, Lz, w);
             inertia_apply(u2, R, J.Ic, mw);
-            T rxf[3], vxl[3];
-            const T wr = dot3(w, r), fw = dot3(ft, w), fr = dot3(ft, r), ww = dot3(w, w);
+            const TV wr = dot3(w, r), fw = dot3(ft, w), ww = dot3(w, w);
+            const TP fr = dot3(ft, r);
             cross3(rxf, r, ft);
             cross3(vxl, v2, Lz);
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 dwb[k] += u1[k] + rxf[k] * m;
-                wb[k] += vxl[k] + u2[k] + (ft[k] * wr + r[k] * fw - T(2.0) * fr * w[k]) * m;
+                wb[k] += vxl[k] + u2[k] + (ft[k] * wr + r[k] * fw - 2.0 * fr * w[k]) * m;
                 ab[k] += ft[k] * m;
             }
-            T r1[3], r2[3], r3[3], r4[3], fxd[3];
+            TV r1[3], r2[3], r3[3], r4[3], fxd[3];
             cross3(r1, v1, Lz);
             cross3(r2, u1, dw);
             cross3(r3, v2, mw);
@@ -251,15 +262,15 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 G[k] += r1[k] + r2[k] + r3[k] + r4[k];
-                T rb = (fxd[k] + w[k] * fw - ww * ft[k]) * m;
+                TV rb = (fxd[k] + w[k] * fw - ww * ft[k]) * m;
                 cwb[k] += rb;
                 ob[k] -= rb;
             }
         }
         // ---- recurrences of joint i: w_i = w_p + zq, dw_i = dw_p + w_p x zq, a_i = a_p + dw_p x d + w_p x (w_p x d)
-        T zqb[3], wpb[3];
+        TV zqb[3], wpb[3];
         {
-            T t1[3], t2[3];
+            TV t1[3], t2[3];
             cross3(t1, dwb, wp);
             cross3(t2, zq, dwb);
 #pragma unroll
@@ -269,21 +280,21 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
         for (int k = 0; k < 3; k++) zb[k] = zb[k] + zqb[k] * qdi;
         gqdi = dot3(z, zqb);
         if (i > 0) {
-            T dxa[3], axd[3];
+            TV dxa[3], axd[3];
             cross3(dxa, d, ab);
             cross3(axd, ab, dwp);
-            const T wa = dot3(wp, ab), ww = dot3(wp, wp), wd = dot3(wp, d), ad = dot3(ab, d);
+            const TV wa = dot3(wp, ab), ww = dot3(wp, wp), wd = dot3(wp, d), ad = dot3(ab, d);
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 dwb[k] += dxa[k];
                 db[k] = axd[k] + wp[k] * wa - ww * ab[k];
-                wpb[k] = wpb[k] + ab[k] * wd + d[k] * wa - T(2.0) * ad * wp[k];
+                wpb[k] = wpb[k] + ab[k] * wd + d[k] * wa - 2.0 * ad * wp[k];
                 ob[k] += db[k];
             }
         }
         // ---- geometric adjoints -> q_i
         {
-            T t1[3], t2[3], t3[3];
+            TV t1[3], t2[3], t3[3];
             cross3(t1, z, zb);
             cross3(t2, o, ob);
             cross3(t3, cw, cwb);
@@ -292,7 +303,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
                 G[k] += t1[k] + t2[k] + t3[k];
                 Ob[k] += ob[k] + cwb[k];
             }
-            T oxO[3];
+            TV oxO[3];
             cross3(oxO, o, Ob);
             gqi = z[0] * (G[0] - oxO[0]) + z[1] * (G[1] - oxO[1]) + z[2] * (G[2] - oxO[2]);
         }
@@ -306,14 +317,14 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
         em.joint(i, taui, gqi, gqdi);
         if (i > 0) {
             // a_{i-1}; o_{i-1} = o_i - d (a point of link i-2) receives -db in Gamma / Obar of q_{<i}
-            T t1[3], t2[3];
+            TV t1[3], t2[3];
             cross3(t1, dwp, d);
             cross3(t2, wp, d);
             cross3(t2, wp, t2);
 #pragma unroll
             for (int k = 0; k < 3; k++) { a[k] = a[k] - t1[k] - t2[k]; o[k] = o[k] - d[k]; }
             if constexpr (ADJ) {
-                T opxd[3];
+                TV opxd[3];
                 cross3(opxd, o, db);
 #pragma unroll
                 for (int k = 0; k < 3; k++) { G[k] -= opxd[k]; Ob[k] -= db[k]; }
@@ -323,8 +334,8 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
         for (int k = 0; k < 3; k++) { w[k] = wp[k]; dw[k] = dwp[k]; }
         if (i > 0) {
             // R_{i-1} = (R_i E_i^T) RX_i^T, row by row in place; o_{i-1} = o_i - d
-            T A[9];
-            rodrigues_rows(A, R, J.axis, T(0.0) - s, omc);
+            TP A[9];
+            rodrigues_rows(A, R, J.axis, TP(0.0) - s, omc);
 #pragma unroll
             for (int rr = 0; rr < 3; rr++)
 #pragma unroll
@@ -339,7 +350,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
 // (q, qd, Fw) given by the In functor: node_fwd_rev without its adjoint statements.
 template <int NJ, class In, class Emit>
 MF_HD void node_values(const DevModel &M, const DevFrame &F, int fp, const In &in, const double *Fw, Emit &em) {
-    node_fwd_rev<double, NJ, false>(M, F, fp, in, Fw, nullptr, nullptr, em);
+    node_fwd_rev<double, double, NJ, false>(M, F, fp, in, Fw, nullptr, nullptr, em);
 }
 
 template <int NJ> struct ArrIn {  // inputs from plain arrays (global memory or LDS)

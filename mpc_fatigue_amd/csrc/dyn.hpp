@@ -45,6 +45,13 @@ MF_HD Dual operator*(Dual a, double s) { return Dual(a.v * s, a.d * s); }
 MF_HD Dual operator*(double s, Dual a) { return Dual(a.v * s, a.d * s); }
 MF_HD Dual &operator+=(Dual &a, Dual b) { a = a + b; return a; }
 MF_HD Dual &operator-=(Dual &a, Dual b) { a = a - b; return a; }
+// mixed with a constant-tangent (plain double) operand: no work on the zero tangent
+MF_HD Dual operator+(Dual a, double b) { return Dual(a.v + b, a.d); }
+MF_HD Dual operator+(double a, Dual b) { return Dual(a + b.v, b.d); }
+MF_HD Dual operator-(Dual a, double b) { return Dual(a.v - b, a.d); }
+MF_HD Dual operator-(double a, Dual b) { return Dual(a - b.v, -b.d); }
+MF_HD Dual &operator+=(Dual &a, double b) { a.v += b; return a; }
+MF_HD Dual &operator-=(Dual &a, double b) { a.v -= b; return a; }
 
 struct HDual {  // a + b e1 + c e2 + d e1 e2
     double a, b, c, d;
@@ -78,38 +85,42 @@ MF_HD void sincos_t(HDual x, HDual &s, HDual &c) {
 MF_HD double val(double x) { return x; }
 MF_HD double val(Dual x) { return x.v; }
 MF_HD double val(HDual x) { return x.a; }
+MF_HD double dtan(double) { return 0.0; }  // tangent part (0 for a plain double)
+MF_HD double dtan(Dual x) { return x.d; }
 
 // ---------------------------------------------------------------- 3-vectors
-template <class T> MF_HD void cross3(T *o, const T *a, const T *b) {
-    T t0 = a[1] * b[2] - a[2] * b[1];
-    T t1 = a[2] * b[0] - a[0] * b[2];
-    T t2 = a[0] * b[1] - a[1] * b[0];
+// Operand types may differ (a Dual with a plain-double pose quantity, adj.hpp): the result
+// type TO is the caller's.
+template <class TO, class TA, class TB> MF_HD void cross3(TO *o, const TA *a, const TB *b) {
+    TO t0 = a[1] * b[2] - a[2] * b[1];
+    TO t1 = a[2] * b[0] - a[0] * b[2];
+    TO t2 = a[0] * b[1] - a[1] * b[0];
     o[0] = t0; o[1] = t1; o[2] = t2;
 }
-template <class T> MF_HD T dot3(const T *a, const T *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-template <class T> MF_HD void matc_mul(T *O, const T *A, const double *B) {
+template <class TA, class TB> MF_HD auto dot3(const TA *a, const TB *b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+template <class TO, class TA> MF_HD void matc_mul(TO *O, const TA *A, const double *B) {
 #pragma unroll
     for (int r = 0; r < 3; r++)
 #pragma unroll
         for (int c = 0; c < 3; c++) O[3 * r + c] = A[3 * r] * B[c] + A[3 * r + 1] * B[3 + c] + A[3 * r + 2] * B[6 + c];
 }
-template <class T> MF_HD void matc_vec(T *o, const T *A, const double *v) {
+template <class TO, class TA> MF_HD void matc_vec(TO *o, const TA *A, const double *v) {
 #pragma unroll
     for (int r = 0; r < 3; r++) o[r] = A[3 * r] * v[0] + A[3 * r + 1] * v[1] + A[3 * r + 2] * v[2];
 }
-template <class T> MF_HD void mat_vec(T *o, const T *A, const T *v) {
-    T t[3];
+template <class TO, class TA, class TB> MF_HD void mat_vec(TO *o, const TA *A, const TB *v) {
+    TO t[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) t[r] = A[3 * r] * v[0] + A[3 * r + 1] * v[1] + A[3 * r + 2] * v[2];
     o[0] = t[0]; o[1] = t[1]; o[2] = t[2];
 }
-template <class T> MF_HD void matT_vec(T *o, const T *A, const T *v) {
-    T t[3];
+template <class TO, class TA, class TB> MF_HD void matT_vec(TO *o, const TA *A, const TB *v) {
+    TO t[3];
 #pragma unroll
     for (int r = 0; r < 3; r++) t[r] = A[r] * v[0] + A[3 + r] * v[1] + A[6 + r] * v[2];
     o[0] = t[0]; o[1] = t[1]; o[2] = t[2];
 }
-template <class T> MF_HD void cmat_vec(T *o, const double *C, const T *v) {  // constant C times v
+template <class TO, class TB> MF_HD void cmat_vec(TO *o, const double *C, const TB *v) {  // constant C times v
 #pragma unroll
     for (int r = 0; r < 3; r++) o[r] = v[0] * C[3 * r] + v[1] * C[3 * r + 1] + v[2] * C[3 * r + 2];
 }

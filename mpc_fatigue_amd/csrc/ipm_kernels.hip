@@ -122,60 +122,77 @@ template <int NJ> struct ModelLds {
 // columns through LDS to add the Gauss-Newton / barrier term and writes the condensed
 // stage Hessian  H0_k = grad^2 L_k + J^T diag(2 wtau + Sigma_s) J + diag(Sigma_x)
 // (what the Riccati recursion needs at delta_w = delta_c = 0).
-template <int NJ, int NF> struct NodeIn {
-    const double *xq, *xqd;
+// TP = Dual: lane of a q direction (tangent e_v on the angle); TP = double: lane of a qd
+// direction (the pose has no tangent, node_fwd_rev runs it in plain FP64)
+template <int NJ, class TP> struct NodeIn {
+    const double *xqd;
     const double (*sc)[2];  // LDS: sin / cos of the node's joint angles (one evaluation per node, not per lane)
     int v;
-    __device__ __forceinline__ Dual q(int i) const { return Dual(xq[i], v == i ? 1.0 : 0.0); }
     __device__ __forceinline__ Dual qd(int i) const { return Dual(xqd[i], v == NJ + i ? 1.0 : 0.0); }
-    __device__ __forceinline__ void sincos(int i, Dual &s, Dual &c) const {
-        const double sv = sc[i][0], cv = sc[i][1], t = (v == i) ? 1.0 : 0.0;
-        s = Dual(sv, cv * t);
-        c = Dual(cv, -sv * t);
+    __device__ __forceinline__ void sincos(int i, TP &s, TP &c) const {
+        const double sv = sc[i][0], cv = sc[i][1];
+        if constexpr (sizeof(TP) == sizeof(Dual)) {
+            const double t = (v == i) ? 1.0 : 0.0;
+            s = TP(sv, cv * t);
+            c = TP(cv, -sv * t);
+        } else {
+            s = sv;
+            c = cv;
+        }
     }
 };
-template <int NJ, int NF, int NPB, int NV> struct NodeOut {
-    double (*Js)[NJ][NV];  // LDS: Jacobian columns of the block's nodes
-    double (*Hs)[NV][NV];  // LDS: Hessian columns of phi
-    double (*Ts)[NJ];      // LDS: tau values
-    int g, v;
+// Per-lane results of node_fwd_rev, written straight to the node's global arrays: column v of
+// d tau / dw (Jt) and column v of grad^2 phi (raw, into W; k_eval_asm completes W in place).
+template <int NJ, int NF, int NV> struct NodeOut {
+    double *Jt, *W;  // the node's blocks
+    double *Ts;      // LDS: tau values of the node (direction-0 lane)
+    int v;
     const double *fdir;
     double pfv[3], pfd[3];
-    __device__ __forceinline__ void frame(const Dual *p) {
+    template <class TP> __device__ __forceinline__ void frame(const TP *p) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) { pfv[k] = p[k].v; pfd[k] = p[k].d; }
+        for (int k = 0; k < 3; k++) { pfv[k] = val(p[k]); pfd[k] = dtan(p[k]); }
     }
-    __device__ __forceinline__ void force(const Dual *gF) {
+    template <class TP> __device__ __forceinline__ void force(const TP *gF) {
 #pragma unroll
         for (int a = 0; a < NF; a++)
-            Hs[g][2 * NJ + a][v] = fdir[3 * a] * gF[0].d + fdir[3 * a + 1] * gF[1].d + fdir[3 * a + 2] * gF[2].d;
+            W[(2 * NJ + a) * NV + v] = fdir[3 * a] * dtan(gF[0]) + fdir[3 * a + 1] * dtan(gF[1]) + fdir[3 * a + 2] * dtan(gF[2]);
     }
     __device__ __forceinline__ void joint(int i, const Dual &t, const Dual &gq, const Dual &gqd) {
-        Js[g][i][v] = t.d;
-        if (v == 0) Ts[g][i] = t.v;
-        Hs[g][i][v] = gq.d;
-        Hs[g][NJ + i][v] = gqd.d;
+        Jt[i * NV + v] = t.d;
+        if (v == 0) Ts[i] = t.v;
+        W[i * NV + v] = gq.d;
+        W[(NJ + i) * NV + v] = gqd.d;
     }
 };
 
+// Blocks hold one direction class each (blockIdx < nb: q directions, else qd directions) of
+// NPB nodes, NJ lanes per node: a qd lane runs the sweep with a plain-FP64 pose and costs about
+// half a q lane, and a block of one class never waits on the slower class (a block's waves
+// keep their registers until the last one finishes).  Each lane writes its own Jacobian and
+// Hessian columns; k_eval_asm adds the Gauss-Newton / barrier terms.  The q-class lanes also
+// write the force columns (d tau / dF_a = -fdir_a . dp_f/dq_v), the line Jacobian, and the
+// node's tau, line residual and cost.
 template <int NJ, int NF, int NL>
 __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
-                                                   OcpConst C, IpmArrays A, int batch) {
+                                                   OcpConst C, IpmArrays A, int batch, int nb) {
     constexpr int NV = 2 * NJ + NF;
-    constexpr int NVL = 2 * NJ;
     constexpr int NFA = NF > 0 ? NF : 1;
-    constexpr int NPB = 256 / NVL;
+    constexpr int NPB = 4 * (64 / NJ);
     __shared__ ModelLds<NJ> Ml;
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
-    __shared__ double Js[NPB][NJ][NV], Hs[NPB][NV][NV], Ts[NPB][NJ], Cs[NPB][NJ];
+    __shared__ double Ts[NPB][NJ], Cs[NPB][NJ];
     __shared__ double SCs[NPB][NJ][2];  // sin / cos of each node's joint angles
     Ml.load(Mg);
     stage_lds(&F, Fg);
-    const int tid = threadIdx.x, g = tid / NVL, v = tid % NVL;
+    const int cls = blockIdx.x < (unsigned)nb ? 0 : 1;
+    const int grp = cls == 0 ? blockIdx.x : blockIdx.x - nb;
+    const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
+    const int g = wv * (64 / NJ) + ln / NJ, j0 = ln % NJ, v = cls * NJ + j0;
     const int N = C.N;
-    const long node = (long)blockIdx.x * NPB + g;
-    bool run = (g < NPB) && node < (long)batch * N;
+    const long node = (long)grp * NPB + g;
+    bool run = (ln < (64 / NJ) * NJ) && node < (long)batch * N;
     int b = 0, k = 0;
     if (run) {
         b = (int)(node / N);
@@ -186,16 +203,15 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     const double *q = A.q + b * S.q + (size_t)k * NJ;
     const double *qd = A.qd + b * S.u + (size_t)k * NJ;
     const double *Fv = A.F + b * S.f + (size_t)k * NFA;
-    NodeOut<NJ, NF, NPB, NV> out;
-    out.Js = Js;
-    out.Hs = Hs;
-    out.Ts = Ts;
-    out.g = g;
+    NodeOut<NJ, NF, NV> out;
+    out.Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
+    out.W = A.W + b * S.w + (size_t)k * NV * NV;
+    out.Ts = Ts[g];
     out.v = v;
     out.fdir = C.fdir;
-    if (run && v < NJ) sincos(q[v], &SCs[g][v][0], &SCs[g][v][1]);
+    if (run) sincos(q[j0], &SCs[g][j0][0], &SCs[g][j0][1]);
     // torque weights c = y_tau + 2 wtau tau (tau at the iterate first when wtau != 0)
-    if (run && v == 0) {
+    if (run && j0 == 0) {
         const double *yd = A.yd + b * S.u + (size_t)k * NJ;
         if (C.wtau != 0.0) {
             struct WOut {
@@ -222,99 +238,39 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
         }
     }
     __syncthreads();
-    if (run) {
-        double yl3[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-        for (int l = 0; l < NL; l++) yl3[l] = A.yl[b * S.l + (size_t)k * NL + l];
-        Dual Fw[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-            Dual acc(0.0);
-#pragma unroll
-            for (int a = 0; a < NF; a++) acc += Dual(Fv[a], v == 2 * NJ + a ? 1.0 : 0.0) * C.fdir[3 * a + r];
-            Fw[r] = acc;
-        }
-        const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
-        NodeIn<NJ, NF> in{q, qd, SCs[g], v};
-        node_fwd_rev<Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
-        // force columns: d tau_v / dF_a = -fdir_a . dp_f/dq_v (q lanes), H_FF = 0
-        if (v < NJ)
-#pragma unroll
-            for (int a = 0; a < NF; a++)
-                Js[g][v][2 * NJ + a] = -(C.fdir[3 * a] * out.pfd[0] + C.fdir[3 * a + 1] * out.pfd[1] +
-                                         C.fdir[3 * a + 2] * out.pfd[2]);
-        if (v == 0)
-#pragma unroll
-            for (int a = 0; a < NF; a++)
-#pragma unroll
-                for (int c2 = 0; c2 < NF; c2++) Hs[g][2 * NJ + a][2 * NJ + c2] = 0.0;
-    }
-    __syncthreads();
     if (!run) return;
-    // barrier Hessian of the node: Sigma_s (torque slacks), Sigma_x (q_k, qd_k bounds, k >= 1)
-    const double *tlo = A.tau_lo + (size_t)k * NJ, *thi = A.tau_hi + (size_t)k * NJ;
-    const double *sk = A.s + b * S.u + (size_t)k * NJ;
-    const double *vL = A.vL + b * S.u + (size_t)k * NJ, *vU = A.vU + b * S.u + (size_t)k * NJ;
-    double wj[NJ];
+    double yl3[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-    for (int j = 0; j < NJ; j++) wj[j] = 2.0 * C.wtau + sigma_pair(vL[j], vU[j], sk[j], tlo[j], thi[j]);
-    double diag = 0.0;
-    if (k > 0) {
-        if (v < NJ) {
-            const size_t e = b * S.q + (size_t)k * NJ + v;
-            diag = sigma_pair(A.zqL[e], A.zqU[e], q[v], C.q_lo[v], C.q_hi[v]);
-        } else if (v < 2 * NJ) {
-            const size_t e = b * S.u + (size_t)k * NJ + v - NJ;
-            diag = sigma_pair(A.zdL[e], A.zdU[e], qd[v - NJ], C.qd_lo[v - NJ], C.qd_hi[v - NJ]);
-        }
+    for (int l = 0; l < NL; l++) yl3[l] = A.yl[b * S.l + (size_t)k * NL + l];
+    double Fw[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < NF; a++) acc += Fv[a] * C.fdir[3 * a + r];
+        Fw[r] = acc;
     }
-    if (v >= NJ && v < 2 * NJ) diag += 2.0 * C.wqd;
-    double *W = A.W + b * S.w + (size_t)k * NV * NV;
-    // entry (u, c) = (c, u) of H0, u >= c
-    auto went = [&](int u, int c, double dg) {
-        double gn = 0.0;
-#pragma unroll
-        for (int j = 0; j < NJ; j++) gn += wj[j] * Js[g][j][u] * Js[g][j][c];
-        double hh = Hs[g][u][c] + gn;
-        if (u == c) hh += dg;
-        W[u * NV + c] = hh;
-        W[c * NV + u] = hh;
-    };
-#pragma unroll
-    for (int u = 0; u < NV; u++)
-        if (u >= v) went(u, v, diag);
-    if (v == 0)  // force-force block (no lane of its own)
-#pragma unroll
-        for (int a = 0; a < NF; a++)
-#pragma unroll
-            for (int c2 = 0; c2 <= a; c2++) went(2 * NJ + a, 2 * NJ + c2, 2.0 * C.wF);
-    double *Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
-    double gfv = 0.0;
-#pragma unroll
-    for (int j = 0; j < NJ; j++) {
-        const double jv = Js[g][j][v];
-        Jt[j * NV + v] = jv;
-        gfv += 2.0 * C.wtau * Ts[g][j] * jv;
+    const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
+    if (cls == 0) {
+        NodeIn<NJ, Dual> in{qd, SCs[g], v};
+        node_fwd_rev<Dual, Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
+    } else {
+        NodeIn<NJ, double> in{qd, SCs[g], v};
+        node_fwd_rev<double, Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
     }
-    if (v >= NJ && v < 2 * NJ) gfv += 2.0 * C.wqd * qd[v - NJ];
-    A.gf[b * S.gf + (size_t)k * NV + v] = gfv;
-    if (v < NJ)
+    if (cls != 0) return;
+    // ---- q lanes: force columns of d tau / dw, line Jacobian column; node values (lane 0)
 #pragma unroll
-        for (int a = 0; a < NF; a++) Jt[v * NV + 2 * NJ + a] = Js[g][v][2 * NJ + a];
-    if (v == 0)
-#pragma unroll
-        for (int a = 0; a < NF; a++) {
-            double ga = 2.0 * C.wF * Fv[a];
-#pragma unroll
-            for (int j = 0; j < NJ; j++) ga += 2.0 * C.wtau * Ts[g][j] * Js[g][j][2 * NJ + a];
-            A.gf[b * S.gf + (size_t)k * NV + 2 * NJ + a] = ga;
-        }
-    if (NL > 0 && v < NJ) {
+    for (int a = 0; a < NF; a++)
+        out.Jt[v * NV + 2 * NJ + a] = -(C.fdir[3 * a] * out.pfd[0] + C.fdir[3 * a + 1] * out.pfd[1] +
+                                        C.fdir[3 * a + 2] * out.pfd[2]);
+    if (NL > 0) {
         double *Jl = A.Jl + b * S.jl + (size_t)k * NL * NJ;
 #pragma unroll
         for (int l = 0; l < NL; l++) Jl[l * NJ + v] = out.pfd[l];
     }
     if (v == 0) {
+        __builtin_amdgcn_wave_barrier();
         double *tvo = A.tau + b * S.u + (size_t)k * NJ;
         double c = 0.0;
 #pragma unroll
@@ -332,6 +288,78 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
             for (int l = 0; l < NL; l++) lv[l] = out.pfv[l] - A.lref[b * 2 + l];
         }
     }
+}
+
+// Completes the condensed stage Hessian in place:
+//   H0_k = grad^2 L_k + J^T diag(2 wtau + Sigma_s) J + diag(Sigma_x) (+ cost curvature)
+// from the raw Hessian columns k_eval_node left in W (lower triangle read, both written) and the
+// Jacobian Jt; also the cost gradient gf.  One lane per (node, column v), NV lanes per node.
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(256) void k_eval_asm(OcpConst C, IpmArrays A, int batch) {
+    constexpr int NV = 2 * NJ + NF;
+    constexpr int NFA = NF > 0 ? NF : 1;
+    constexpr int NPB = 256 / NV;
+    __shared__ double Js[NPB][NJ][NV], Wj[NPB][NJ];
+    const int tid = threadIdx.x, g = tid / NV, v = tid % NV;
+    const int N = C.N;
+    const long node = (long)blockIdx.x * NPB + g;
+    bool run = g < NPB && node < (long)batch * N;
+    int b = 0, k = 0;
+    if (run) {
+        b = (int)(node / N);
+        k = (int)(node % N);
+        run = A.st[b].status == ST_RUNNING;
+    }
+    const IpmSizes S = ipm_sizes(C);
+    const double *Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
+    double *W = A.W + b * S.w + (size_t)k * NV * NV;
+    const double *q = A.q + b * S.q + (size_t)k * NJ, *qd = A.qd + b * S.u + (size_t)k * NJ;
+    const double *Fv = A.F + b * S.f + (size_t)k * NFA;
+    double raw[NV];
+    if (run) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) Js[g][j][v] = Jt[j * NV + v];
+        if (v < NJ) {
+            const size_t e = b * S.u + (size_t)k * NJ + v;
+            Wj[g][v] = 2.0 * C.wtau + sigma_pair(A.vL[e], A.vU[e], A.s[e], A.tau_lo[(size_t)k * NJ + v],
+                                                 A.tau_hi[(size_t)k * NJ + v]);
+        }
+#pragma unroll
+        for (int u = 0; u < NV; u++) raw[u] = (u >= v) ? W[u * NV + v] : 0.0;
+    }
+    __syncthreads();
+    if (!run) return;
+    double diag = 0.0;
+    if (k > 0) {
+        if (v < NJ) {
+            const size_t e = b * S.q + (size_t)k * NJ + v;
+            diag = sigma_pair(A.zqL[e], A.zqU[e], q[v], C.q_lo[v], C.q_hi[v]);
+        } else if (v < 2 * NJ) {
+            const size_t e = b * S.u + (size_t)k * NJ + v - NJ;
+            diag = sigma_pair(A.zdL[e], A.zdU[e], qd[v - NJ], C.qd_lo[v - NJ], C.qd_hi[v - NJ]);
+        }
+    }
+    if (v >= NJ && v < 2 * NJ) diag += 2.0 * C.wqd;
+    if (v >= 2 * NJ) diag += 2.0 * C.wF;
+    // phi is linear in F: the force-force block of the raw Hessian is zero (no lane computed it)
+#pragma unroll
+    for (int u = 0; u < NV; u++) {
+        if (u < v) continue;
+        double gn = 0.0;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) gn += Wj[g][j] * Js[g][j][u] * Js[g][j][v];
+        double hh = ((u >= 2 * NJ && v >= 2 * NJ) ? 0.0 : raw[u]) + gn;
+        if (u == v) hh += diag;
+        W[u * NV + v] = hh;
+        W[v * NV + u] = hh;
+    }
+    const double *tv = A.tau + b * S.u + (size_t)k * NJ;
+    double gfv = 0.0;
+#pragma unroll
+    for (int j = 0; j < NJ; j++) gfv += 2.0 * C.wtau * tv[j] * Js[g][j][v];
+    if (v >= NJ && v < 2 * NJ) gfv += 2.0 * C.wqd * qd[v - NJ];
+    if (NF > 0 && v >= 2 * NJ) gfv += 2.0 * C.wF * Fv[v - 2 * NJ];
+    A.gf[b * S.gf + (size_t)k * NV + v] = gfv;
 }
 
 // ============================================================== init
@@ -1712,11 +1740,15 @@ struct IpmLaunch {
     // phase 0: node derivatives (k_eval_node), 1..3: per-problem IPM phases (k_ipm_pre, k_ipm_kkt, k_ipm_post)
     static void iter(int phase, const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A,
                      int batch, hipStream_t s) {
-        constexpr int NPB = 256 / (2 * NJ);  // k_eval_node: 2 NJ lanes per node
+        constexpr int NPB = 4 * (64 / NJ);        // k_eval_node: nodes per block (one direction class)
+        constexpr int NPBA = 256 / (2 * NJ + NF);  // k_eval_asm: nodes per block
         long nodes = (long)batch * C.N;
-        if (phase == 0)
-            hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3((unsigned)((nodes + NPB - 1) / NPB)), dim3(256), 0, s,
-                               M, F, C, A, batch);
+        if (phase == 0) {
+            const int nb = (int)((nodes + NPB - 1) / NPB);
+            hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3(2 * nb), dim3(256), 0, s, M, F, C, A, batch, nb);
+            hipLaunchKernelGGL((k_eval_asm<NJ, NF, NL>), dim3((unsigned)((nodes + NPBA - 1) / NPBA)), dim3(256), 0, s,
+                               C, A, batch);
+        }
         else {
             if (phase == 1) hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
             else if (phase == 2) hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
