@@ -1,6 +1,6 @@
-// Test harness (CPU): runs the device template node_fwd_rev<Dual, n> of
+// Test harness (CPU): runs the device template node_fwd_rev of
 // mpc_fatigue_amd/csrc/adj.hpp on the host, one tangent direction at a time,
-// exactly as the GPU kernel's 13 lanes per node do.  Used by
+// exactly as the GPU kernel's 2n lanes per node do (force columns derived).  Used by
 // tests/test_adjoint_cpu.py to check the forward-over-reverse Hessian against
 // the oracle's hyper-dual one without a GPU.  Not part of the product library.
 #include <cstring>
@@ -11,17 +11,26 @@
 
 using namespace mf;
 
-template <int NJ> struct In {
+// Lanes of a q direction run TP = Dual (the angle carries the tangent), lanes of a qd direction
+// TP = double (plain-FP64 pose), exactly as k_eval_node's two block classes do.
+template <int NJ, class TP> struct In {
     const double *xq, *xqd;
     int v;
-    Dual q(int i) const { return Dual(xq[i], v == i ? 1.0 : 0.0); }
     Dual qd(int i) const { return Dual(xqd[i], v == NJ + i ? 1.0 : 0.0); }
+    void sincos(int i, TP &s, TP &c) const {
+        if constexpr (sizeof(TP) == sizeof(Dual)) {
+            sincos_t(Dual(xq[i], v == i ? 1.0 : 0.0), s, c);
+        } else {
+            sincos_t(xq[i], s, c);
+        }
+    }
 };
 
 template <int NJ> struct Out {
-    Dual tau[NJ], gq[NJ], gqd[NJ], pf[3], gF[3];
-    void frame(const Dual *p) { for (int k = 0; k < 3; k++) pf[k] = p[k]; }
-    void force(const Dual *g) { for (int k = 0; k < 3; k++) gF[k] = g[k]; }
+    Dual tau[NJ], gq[NJ], gqd[NJ];
+    double pfv[3], pfd[3], gFd[3];
+    template <class TP> void frame(const TP *p) { for (int k = 0; k < 3; k++) { pfv[k] = val(p[k]); pfd[k] = dtan(p[k]); } }
+    template <class TP> void force(const TP *g) { for (int k = 0; k < 3; k++) gFd[k] = dtan(g[k]); }
     void joint(int i, const Dual &t, const Dual &a, const Dual &b) { tau[i] = t; gq[i] = a; gqd[i] = b; }
 };
 
@@ -30,30 +39,44 @@ static void run(const DevModel &M, const DevFrame &F, int fp, int nf, const doub
                 const double *qd, const double *Fv, const double *c, const double *yl3, double *tau, double *Jt,
                 double *pf, double *Jp, double *H) {
     const int nv = 2 * NJ + nf;
-    for (int v = 0; v < nv; v++) {
-        In<NJ> in{q, qd, v};
+    double Fw[3];
+    for (int k = 0; k < 3; k++) {
+        double acc = 0.0;
+        for (int a = 0; a < nf; a++) acc += Fv[a] * fdir[3 * a + k];
+        Fw[k] = acc;
+    }
+    for (int v = 0; v < 2 * NJ; v++) {
         Out<NJ> o;
-        Dual Fw[3];
-        for (int k = 0; k < 3; k++) {
-            Dual acc(0.0);
-            for (int a = 0; a < nf; a++) acc += Dual(Fv[a], v == 2 * NJ + a ? 1.0 : 0.0) * fdir[3 * a + k];
-            Fw[k] = acc;
+        if (v < NJ) {
+            In<NJ, Dual> in{q, qd, v};
+            node_fwd_rev<Dual, Dual, NJ>(M, F, fp, in, Fw, c, yl3, o);
+        } else {
+            In<NJ, double> in{q, qd, v};
+            node_fwd_rev<double, Dual, NJ>(M, F, fp, in, Fw, c, yl3, o);
         }
-        node_fwd_rev<Dual, NJ>(M, F, fp, in, Fw, c, yl3, o);
         for (int j = 0; j < NJ; j++) Jt[j * nv + v] = o.tau[j].d;
-        if (v < NJ)
-            for (int k = 0; k < 3; k++) Jp[k * NJ + v] = o.pf[k].d;
+        if (v < NJ) {
+            for (int k = 0; k < 3; k++) Jp[k * NJ + v] = o.pfd[k];
+            // force column: d tau_v / dF_a = -fdir_a . dp_f/dq_v
+            for (int a = 0; a < nf; a++)
+                Jt[v * nv + 2 * NJ + a] = -(fdir[3 * a] * o.pfd[0] + fdir[3 * a + 1] * o.pfd[1] + fdir[3 * a + 2] * o.pfd[2]);
+        }
         if (v == 0) {
             for (int j = 0; j < NJ; j++) tau[j] = o.tau[j].v;
-            for (int k = 0; k < 3; k++) pf[k] = o.pf[k].v;
+            for (int k = 0; k < 3; k++) pf[k] = o.pfv[k];
         }
         for (int u = 0; u < NJ; u++) {
             H[u * nv + v] = o.gq[u].d;
             H[(NJ + u) * nv + v] = o.gqd[u].d;
         }
-        for (int a = 0; a < nf; a++)
-            H[(2 * NJ + a) * nv + v] = fdir[3 * a] * o.gF[0].d + fdir[3 * a + 1] * o.gF[1].d + fdir[3 * a + 2] * o.gF[2].d;
+        for (int a = 0; a < nf; a++) {
+            const double hv = fdir[3 * a] * o.gFd[0] + fdir[3 * a + 1] * o.gFd[1] + fdir[3 * a + 2] * o.gFd[2];
+            H[(2 * NJ + a) * nv + v] = hv;
+            H[v * nv + 2 * NJ + a] = hv;  // symmetry: the force columns have no lane of their own
+        }
     }
+    for (int a = 0; a < nf; a++)
+        for (int b = 0; b < nf; b++) H[(2 * NJ + a) * nv + 2 * NJ + b] = 0.0;  // phi is linear in F
 }
 
 extern "C" int adj_node(const char *urdf, const char *frame, int nf, const double *fdir, int nl, const double *q,
