@@ -38,22 +38,19 @@ FP64_PEAK_TFS = 78.6          # MI355X FP64 vector peak (spec)
 def node_bytes(n: int, nf: int, nl: int) -> dict:
     """Algorithmic HBM bytes per shooting node of one running horizon per launch.
 
-    k_eval_node: reads the node's q, qd, F, y_tau, y_line, torque slacks and their
-                 multipliers, the fatigue bounds and the q/qd bound multipliers; writes
-                 tau, line, cost, d tau/dw, d line/dq, grad f and the condensed stage
-                 Hessian H0 (nv x nv)
-    k_ipm_iter : reads the node data once (H0, d tau/dw, grad f, tau, line, dline/dq, cost),
-                 reads and writes the iterate once (q, qd, F, s, y_c, y_line, y_tau, 4
-                 bound-multiplier sets, 2 slack-multiplier sets), writes and reads back the
-                 Riccati slot once (Ku, Kl, P_{k+1}, ku, kl, p_{k+1})
+    k_eval_node: reads q, qd, F, y_tau, y_line of the node; writes d tau/dw (n x nv), the raw
+                 Hessian columns of the 2n lane directions (nv x 2n), d line/dq, tau, line, cost
+    k_eval_asm : reads the raw Hessian's lower triangle, d tau/dw, the torque-slack and bound
+                 multiplier data of the node; writes the condensed stage Hessian H0 and grad f
+    k_ipm_kkt  : reads H0, d tau/dw, grad f and the stage data once, writes and reads back the
+                 Riccati slot (Ku, Kl, P_{k+1}, ku, kl, p_{k+1}) and the step
     """
-    nv, nu = 2 * n + nf, n + nf
-    rd = (n + n + nf) + n + nl + 3 * n + 2 * n + 4 * n
-    wr = n + nl + 1 + n * nv + nl * n + nv + nv * nv
-    node = nv * nv + n * nv + nv + n + nl + nl * n + 1
-    state = (n + n + nf + n + n + nl + n) + 2 * n + 2 * n + 2 * n
+    nv, nu, nla = 2 * n + nf, n + nf, max(nl, 1)
+    ev = (2 * n + nf + n + nl) + (n * nv + nv * 2 * n + nl * n + n + nl + 1)
+    asm = (nv * (nv + 1) // 2 + n * nv + 3 * n + 2 * n + 6 * n + n + nf) + (nv * nv + nv)
     slot = nu * n + nl * n + n * n + nu + nl + n
-    return {"k_eval_node": 8 * (rd + wr), "k_ipm_iter": 8 * (node + 2 * state + 2 * slot)}
+    kkt = (nv * nv + n * nv + nv + n + nla + nl * n) + 2 * slot + (2 * n + nf + n + nl + n) + (2 * n + nv + 2 * n + nla)
+    return {"k_eval_node": 8 * ev, "k_eval_asm": 8 * asm, "k_ipm_kkt": 8 * kkt}
 
 
 def main() -> int:
@@ -153,16 +150,23 @@ def main() -> int:
         bytes_per_launch = total_bytes / max(1, dom_launches)
     else:
         achieved, bytes_per_launch = None, None
-    traffic = None
+    traffic, fp64 = None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
-            traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+            pmc = json.load(f).get(dom, {})
+        traffic = pmc.get("hbm_bytes_per_launch")
+        if pmc.get("fp64_flops_per_launch"):
+            # executed FP64 flops per launch (PMC, same workload) over this run's launch time
+            tfs = pmc["fp64_flops_per_launch"] / (per_launch_ms / 1e3) / 1e12
+            fp64 = {"achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / FP64_PEAK_TFS,
+                    "flops_per_launch": pmc["fp64_flops_per_launch"],
+                    "note": "FP64 VALU work (the bound of this kernel); flops from SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 x 64 lanes"}
     roofline = {
         "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
         "avg_launch_ms": per_launch_ms, "launches": dom_launches, "algorithmic_bytes_per_launch": bytes_per_launch,
-        "kernel_ms": {k: v[0] for k, v in stats.items()},
+        "kernel_ms": {k: v[0] for k, v in stats.items()}, "fp64": fp64,
     }
 
     result = {

@@ -128,11 +128,11 @@ int mf_solve_batch_dev(mf_problem *p, int batch, const double *q0, const double 
 
 /* Per-kernel device time of the solver's launches on the solve stream (HIP events),
  * MF_NKERNELS slots named by mf_kernel_name(slot), in launch order of one interior-point
- * iteration: 0 = node values, Jacobians and condensed stage Hessians (k_eval_node, k_eval_asm),
- * 1 = optimality error and barrier terms (k_ipm_pre), 2 = inertia-corrected Riccati
- * recursion and step recovery (k_ipm_kkt), 3 = line search and update (k_ipm_post).
- * Enabling resets the totals. */
-#define MF_NKERNELS 4
+ * iteration: 0 = node values, Jacobian and Hessian columns (k_eval_node), 1 = condensed
+ * stage Hessians and cost gradients (k_eval_asm), 2 = optimality error and barrier terms
+ * (k_ipm_pre), 3 = inertia-corrected Riccati recursion and step recovery (k_ipm_kkt),
+ * 4 = line search and update (k_ipm_post).  Enabling resets the totals. */
+#define MF_NKERNELS 5
 int mf_problem_timing(mf_problem *p, int enable);
 int mf_problem_kernel_stats(const mf_problem *p, double *ms_total, long *launches);
 const char *mf_kernel_name(int slot);

@@ -16,7 +16,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libmpcfatigue.so")
 MF_MAX_JOINTS = 16
-MF_NKERNELS = 4
+MF_NKERNELS = 5
 
 MF_ERR = {0: "OK", -1: "ARG", -2: "URDF", -3: "FRAME", -4: "DEVICE", -5: "UNSUPPORTED", -6: "NOMEM"}
 

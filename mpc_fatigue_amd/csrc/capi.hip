@@ -468,7 +468,7 @@ static int solve_core(mf_problem *p, int batch, const double *d_q0, const double
         return fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
     HIPCHK(hipGetLastError());
     int active = batch;
-    const int chunk = 4, NPH = 4;  // launches per iteration: k_eval_node, k_ipm_pre, k_ipm_kkt, k_ipm_post
+    const int chunk = 4, NPH = 5;  // launches per iteration: k_eval_node, k_eval_asm, k_ipm_pre, k_ipm_kkt, k_ipm_post
     if (p->timing && p->ev.size() < (size_t)(2 * NPH * chunk)) {
         for (auto e2 : p->ev) (void)hipEventDestroy(e2);
         p->ev.assign(2 * NPH * chunk, nullptr);
@@ -640,7 +640,7 @@ extern "C" int mf_problem_timing(mf_problem *p, int enable) {
 }
 
 extern "C" const char *mf_kernel_name(int slot) {
-    static const char *names[MF_NKERNELS] = {"k_eval_node", "k_ipm_pre", "k_ipm_kkt", "k_ipm_post"};
+    static const char *names[MF_NKERNELS] = {"k_eval_node", "k_eval_asm", "k_ipm_pre", "k_ipm_kkt", "k_ipm_post"};
     return (slot >= 0 && slot < MF_NKERNELS) ? names[slot] : "";
 }
 

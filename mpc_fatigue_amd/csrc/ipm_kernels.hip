@@ -1737,7 +1737,8 @@ struct IpmLaunch {
                      hipStream_t s) {
         hipLaunchKernelGGL((k_ipm_init<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
     }
-    // phase 0: node derivatives (k_eval_node), 1..3: per-problem IPM phases (k_ipm_pre, k_ipm_kkt, k_ipm_post)
+    // phase 0: node derivatives (k_eval_node), 1: stage-Hessian assembly (k_eval_asm),
+    // 2..4: per-problem IPM phases (k_ipm_pre, k_ipm_kkt, k_ipm_post)
     static void iter(int phase, const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A,
                      int batch, hipStream_t s) {
         constexpr int NPB = 4 * (64 / NJ);        // k_eval_node: nodes per block (one direction class)
@@ -1746,13 +1747,15 @@ struct IpmLaunch {
         if (phase == 0) {
             const int nb = (int)((nodes + NPB - 1) / NPB);
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3(2 * nb), dim3(256), 0, s, M, F, C, A, batch, nb);
+        } else if (phase == 1) {
             hipLaunchKernelGGL((k_eval_asm<NJ, NF, NL>), dim3((unsigned)((nodes + NPBA - 1) / NPBA)), dim3(256), 0, s,
                                C, A, batch);
-        }
-        else {
-            if (phase == 1) hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
-            else if (phase == 2) hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
-            else hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+        } else if (phase == 2) {
+            hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+        } else if (phase == 3) {
+            hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+        } else {
+            hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
         }
     }
     static void output(const OcpConst &C, const IpmArrays &A, int batch, double *w, int *status, int *iters,
@@ -1773,7 +1776,7 @@ bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevF
 #define MF_CASE(NJ, NF, NL)                                                       \
     if (n == NJ && nf == NF && nl == NL) {                                        \
         if (what == 0) IpmLaunch<NJ, NF, NL>::init(M, F, C, A, batch, s);          \
-        else if (what >= 10 && what <= 13) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
+        else if (what >= 10 && what <= 14) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
         else IpmLaunch<NJ, NF, NL>::output(C, A, batch, w, status, iters, kkt, obj, s); \
         return true;                                                              \
     }

@@ -2,7 +2,9 @@
 MI355X_MICROARCH.md HBM section), calibrated on the copy kernel of tools/traffic_run.py (known
 512 MiB read + 512 MiB written), written to profiles/pmc_traffic.json for bench.py.
 
-usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV [OUT_JSON]
+usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV [OUT_JSON [FP64_CSV]]
+FP64_CSV (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 pass) adds executed FP64 flops per launch:
+64 lanes x (2 FMA + MUL + ADD) per wave instruction, an upper bound (masked lanes count).
 """
 import csv
 import json
@@ -27,6 +29,13 @@ def main():
     fetch = load(sys.argv[1], "FETCH_SIZE")
     write = load(sys.argv[2], "WRITE_SIZE")
     out_path = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    flops = {}
+    if len(sys.argv) > 4:
+        fma, mul, add = (load(sys.argv[4], c) for c in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                        "SQ_INSTS_VALU_ADD_F64"))
+        for k in fma:
+            n = max(len(fma[k]), 1)
+            flops[k] = 64.0 * (2.0 * sum(fma[k]) + sum(mul.get(k, [])) + sum(add.get(k, []))) / n
     # calibration: the largest elementwise (copy) dispatch moved exactly COPY_BYTES each way
     cal_keys = [k for k in fetch if "elementwise" in k or "copy" in k.lower()]
     fr = max(v for k in cal_keys for v in fetch[k])
@@ -43,6 +52,8 @@ def main():
         wt = sum(wv) * w_scale / max(len(wv), 1)
         res[k] = {"launches": len(fv), "read_bytes_per_launch": rd, "write_bytes_per_launch": wt,
                   "hbm_bytes_per_launch": rd + wt}
+        if k in flops:
+            res[k]["fp64_flops_per_launch"] = flops[k]
     json.dump(res, open(out_path, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
