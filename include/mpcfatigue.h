@@ -126,6 +126,18 @@ int mf_solve_batch_dev(mf_problem *p, int batch, const double *q0, const double 
                        const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt, double *obj,
                        void *stream);
 
+/* Batched inverse kinematics of a frame position.  Replaces the per-script IPOPT solve of
+ * min ||fk(q) - p||^2 from q = 0 (python/Pilz_6_DOF/force_optimization_pilz_6DOF.py:55-63,
+ * python/2_pilz_6_DOF/Box_Pilz_6DOF.py:123-156, Centauro_functions.py:207-260) that produces
+ * each script's initial state: damped least squares (J J^T + lam I) y = e, dq = J^T y, steps
+ * capped at max_step (max norm), stop when |p - fk(q)| < tol or after iters steps.
+ * target: batch x 3; q_init: batch x n or NULL (q = 0, as the reference); q_out: batch x n;
+ * residual: batch (|p - fk(q_out)|, may be NULL).  _dev: device pointers, async on stream. */
+int mf_ik_batch(const mf_model *m, int frame, const double *target, const double *q_init, double *q_out,
+                double *residual, int batch, int iters, double lam, double max_step, double tol);
+int mf_ik_batch_dev(const mf_model *m, int frame, const double *target, const double *q_init, double *q_out,
+                    double *residual, int batch, int iters, double lam, double max_step, double tol, void *stream);
+
 /* Per-kernel device time of the solver's launches on the solve stream (HIP events),
  * MF_NKERNELS slots named by mf_kernel_name(slot), in launch order of one interior-point
  * iteration: 0 = node values, Jacobian and Hessian columns (k_eval_node), 1 = condensed

@@ -258,6 +258,100 @@ extern "C" int mf_jac_dev(const mf_model *m, int frame, const double *q, double 
     return kin_dev(m, frame, q, nullptr, nullptr, J, batch, stream);
 }
 
+// ====================================================================== batched IK
+// The reference solves min ||fk(q) - p||^2 with IPOPT from q = 0 once per script
+// (force_optimization_pilz_6DOF.py:55-63, Box_Pilz_6DOF.py:123-156).  Here one lane per target
+// runs damped least squares on the frame position: e = p - fk(q), (J J^T + lam I) y = e
+// (3 x 3 Cholesky), dq = J^T y, the step capped at max_step in the max norm so the iterate
+// stays on the branch nearest its start; stop at |e| < tol.  Same iteration as the fixture
+// generator tests/golden/make_fixtures.py:ik (numpy), which pins it.
+template <int NJ>
+__global__ __launch_bounds__(256) void k_ik(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                            const double *target, const double *q_init, double *q_out,
+                                            double *residual, int batch, int iters, double lam, double max_step,
+                                            double tol) {
+    __shared__ DevModel M;
+    __shared__ DevFrame F;
+    {
+        const double *s = reinterpret_cast<const double *>(Mg);
+        double *d = reinterpret_cast<double *>(&M);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevModel) / sizeof(double)); i += blockDim.x) d[i] = s[i];
+        const double *s2 = reinterpret_cast<const double *>(Fg);
+        double *d2 = reinterpret_cast<double *>(&F);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevFrame) / sizeof(double)); i += blockDim.x) d2[i] = s2[i];
+    }
+    __syncthreads();
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    const int n = M.n;
+    double q[NJ], zero[NJ];
+    for (int i = 0; i < n; i++) { q[i] = q_init ? q_init[b * n + i] : 0.0; zero[i] = 0.0; }
+    const double t0 = target[3 * b], t1 = target[3 * b + 1], t2 = target[3 * b + 2];
+    double en = INFINITY;
+    for (int it = 0; it <= iters; it++) {
+        JacVis<double, NJ> jv;
+        jv.F = &F;
+        if (F.parent < 0) {
+            for (int k = 0; k < 3; k++) jv.pf[k] = F.t[k];
+            for (int k = 0; k < 9; k++) jv.Rf[k] = F.R[k];
+        }
+        ne_pass<double>(M, n, q, zero, (const double *)nullptr, jv);
+        const double e[3] = {t0 - jv.pf[0], t1 - jv.pf[1], t2 - jv.pf[2]};
+        en = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+        if (en < tol || it == iters) break;
+        // position Jacobian columns: z_j x (p - o_j) for the frame's ancestors
+        double Jc[NJ][3];
+        for (int j = 0; j < n; j++) {
+            bool anc = false;
+            for (int a = F.parent; a >= 0; a = M.j[a].parent)
+                if (a == j) { anc = true; break; }
+            double d[3] = {jv.pf[0] - jv.o[j][0], jv.pf[1] - jv.o[j][1], jv.pf[2] - jv.o[j][2]};
+            double c[3];
+            cross3(c, jv.z[j], d);
+            for (int k = 0; k < 3; k++) Jc[j][k] = anc ? c[k] : 0.0;
+        }
+        double A[3][3];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double a = (r == c) ? lam : 0.0;
+                for (int j = 0; j < n; j++) a += Jc[j][r] * Jc[j][c];
+                A[r][c] = a;
+            }
+        // Cholesky of the SPD 3 x 3 system
+        const double l00 = sqrt(A[0][0]), l10 = A[1][0] / l00, l20 = A[2][0] / l00;
+        const double l11 = sqrt(A[1][1] - l10 * l10), l21 = (A[2][1] - l20 * l10) / l11;
+        const double l22 = sqrt(A[2][2] - l20 * l20 - l21 * l21);
+        const double z0 = e[0] / l00, z1 = (e[1] - l10 * z0) / l11, z2 = (e[2] - l20 * z0 - l21 * z1) / l22;
+        const double y2 = z2 / l22, y1 = (z1 - l21 * y2) / l11, y0 = (z0 - l10 * y1 - l20 * y2) / l00;
+        double dq[NJ], step = 0.0;
+        for (int j = 0; j < n; j++) {
+            dq[j] = Jc[j][0] * y0 + Jc[j][1] * y1 + Jc[j][2] * y2;
+            step = fmax(step, fabs(dq[j]));
+        }
+        const double sc = (step > max_step) ? max_step / step : 1.0;
+        for (int j = 0; j < n; j++) q[j] += dq[j] * sc;
+    }
+    for (int i = 0; i < n; i++) q_out[b * n + i] = q[i];
+    if (residual) residual[b] = en;
+}
+
+extern "C" int mf_ik_batch_dev(const mf_model *mc, int frame, const double *target, const double *q_init,
+                               double *q_out, double *residual, int batch, int iters, double lam, double max_step,
+                               double tol, void *stream) {
+    mf_model *m = const_cast<mf_model *>(mc);
+    if (!m || !target || !q_out || batch < 0 || iters < 0 || !(lam > 0.0) || !(max_step > 0.0))
+        return fail(MF_ERR_ARG, "bad argument");
+    int e = check_serial(m);
+    if (e) return e;
+    DevFrame *F;
+    if ((e = frame_dev(m, frame, &F))) return e;
+    if (batch == 0) return MF_OK;
+    hipLaunchKernelGGL(k_ik<MF_MAX_JOINTS>, dim3((batch + 255) / 256), dim3(256), 0, (hipStream_t)stream, m->d_model,
+                       F, target, q_init, q_out, residual, batch, iters, lam, max_step, tol);
+    HIPCHK(hipGetLastError());
+    return MF_OK;
+}
+
 // host-pointer wrappers: stage through device buffers
 struct DBuf {
     double *p = nullptr;
@@ -306,6 +400,23 @@ extern "C" int mf_jac(const mf_model *m, int frame, const double *q, double *J, 
     if ((e = h2d(a, q, n)) || (e = dalloc(j, 6 * n))) return e;
     if ((e = mf_jac_dev(m, frame, a.p, j.p, batch, nullptr))) return e;
     HIPCHK(hipMemcpy(J, j.p, 6 * n * sizeof(double), hipMemcpyDeviceToHost));
+    return MF_OK;
+}
+
+extern "C" int mf_ik_batch(const mf_model *m, int frame, const double *target, const double *q_init, double *q_out,
+                           double *residual, int batch, int iters, double lam, double max_step, double tol) {
+    if (!m || !target || !q_out || batch < 0) return fail(MF_ERR_ARG, "null argument");
+    int e = ensure_device();
+    if (e) return e;
+    size_t n = (size_t)m->host.joints.size() * batch;
+    DBuf t, qi, qo, r;
+    if ((e = h2d(t, target, 3 * (size_t)batch)) || (e = dalloc(qo, n)) || (e = dalloc(r, (size_t)batch))) return e;
+    if (q_init && (e = h2d(qi, q_init, n))) return e;
+    if ((e = mf_ik_batch_dev(m, frame, t.p, q_init ? qi.p : nullptr, qo.p, r.p, batch, iters, lam, max_step, tol,
+                             nullptr)))
+        return e;
+    HIPCHK(hipMemcpy(q_out, qo.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    if (residual) HIPCHK(hipMemcpy(residual, r.p, (size_t)batch * sizeof(double), hipMemcpyDeviceToHost));
     return MF_OK;
 }
 
