@@ -138,6 +138,18 @@ int mf_ik_batch(const mf_model *m, int frame, const double *target, const double
 int mf_ik_batch_dev(const mf_model *m, int frame, const double *target, const double *q_init, double *q_out,
                     double *residual, int batch, int iters, double lam, double max_step, double tol, void *stream);
 
+/* Warm-started batch solve (the receding-horizon calls of mpc_principal.py:357-377 and
+ * RepeatedMPCwithThermal.py:445-487: Solver(x0 = sol, ...) with ipopt warm_start_init_point):
+ * qd0 (batch x n, or NULL = the spec's) is each problem's fixed qd_0; w0 (batch x wsize, or NULL
+ * = cold start) supplies q_k, qd_k (k >= 1) and F_k, pushed into their bounds; q_0 is q0.
+ * Multipliers start cold.  w0 must not alias w. */
+int mf_solve_batch_ws(mf_problem *p, int batch, const double *q0, const double *qd0, const double *w0,
+                      const double *line_ref, const mf_solver_opts *opts, double *w, int *status, int *iters,
+                      double *kkt, double *obj, int device);
+int mf_solve_batch_ws_dev(mf_problem *p, int batch, const double *q0, const double *qd0, const double *w0,
+                          const double *line_ref, const mf_solver_opts *opts, double *w, int *status, int *iters,
+                          double *kkt, double *obj, void *stream);
+
 /* Per-kernel device time of the solver's launches on the solve stream (HIP events),
  * MF_NKERNELS slots named by mf_kernel_name(slot), in launch order of one interior-point
  * iteration: 0 = node values, Jacobian and Hessian columns (k_eval_node), 1 = condensed

@@ -83,6 +83,8 @@ def lib() -> C.CDLL:
         "mf_node_eval": ([vp, dp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
         "mf_solve_batch": ([vp, C.c_int, dp, dp, C.POINTER(SolverOpts), dp, ip, ip, dp, dp, C.c_int], C.c_int),
         "mf_solve_batch_dev": ([vp, C.c_int, vp, vp, C.POINTER(SolverOpts), vp, vp, vp, vp, vp, vp], C.c_int),
+        "mf_solve_batch_ws": ([vp, C.c_int, dp, dp, dp, dp, C.POINTER(SolverOpts), dp, ip, ip, dp, dp, C.c_int], C.c_int),
+        "mf_solve_batch_ws_dev": ([vp, C.c_int, vp, vp, vp, vp, C.POINTER(SolverOpts), vp, vp, vp, vp, vp, vp], C.c_int),
         "mf_problem_timing": ([vp, C.c_int], C.c_int),
         "mf_problem_kernel_stats": ([vp, dp, C.POINTER(C.c_long)], C.c_int),
         "mf_kernel_name": ([C.c_int], cp),
@@ -102,7 +104,8 @@ def lib() -> C.CDLL:
 EXPORTED_SYMBOLS = [
     "mf_model_from_urdf", "mf_model_free", "mf_model_nq", "mf_model_export", "mf_frame_id", "mf_frame_export",
     "mf_id", "mf_fk", "mf_jac", "mf_id_dev", "mf_fk_dev", "mf_jac_dev", "mf_problem_create", "mf_problem_free",
-    "mf_problem_wsize", "mf_node_eval", "mf_solve_batch", "mf_solve_batch_dev", "mf_problem_timing",
+    "mf_problem_wsize", "mf_node_eval", "mf_solve_batch", "mf_solve_batch_dev", "mf_solve_batch_ws",
+    "mf_solve_batch_ws_dev", "mf_problem_timing",
     "mf_problem_kernel_stats", "mf_kernel_name", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
 ]
 

@@ -552,7 +552,8 @@ static int ensure_ws(mf_problem *p, int batch) {
     return MF_OK;
 }
 
-static int solve_core(mf_problem *p, int batch, const double *d_q0, const double *d_lref, const mf_solver_opts *o,
+static int solve_core(mf_problem *p, int batch, const double *d_q0, const double *d_qd0, const double *d_w0,
+                      const double *d_lref, const mf_solver_opts *o,
                       double *d_w, int *d_status, int *d_iters, double *d_kkt, double *d_obj, hipStream_t s) {
     int e = ensure_ws(p, batch);
     if (e) return e;
@@ -563,6 +564,8 @@ static int solve_core(mf_problem *p, int batch, const double *d_q0, const double
     C.mu_init = o ? o->mu_init : 0.1;
     C.F_init = o ? o->F_init : 0.0;
     IpmArrays A = p->A;
+    A.qd0p = d_qd0;
+    A.w0 = d_w0;
     const int n = C.n;
     HIPCHK(hipMemcpyAsync(A.q0, d_q0, sizeof(double) * n * (size_t)batch, hipMemcpyDeviceToDevice, s));
     if (d_lref) {
@@ -617,25 +620,27 @@ extern "C" int mf_solve_batch_dev(mf_problem *p, int batch, const double *q0, co
     if (!p || !q0 || !w || batch < 1) return fail(MF_ERR_ARG, "bad argument");
     int e = ensure_device();
     if (e) return e;
-    return solve_core(p, batch, q0, line_ref, opts, w, status, iters, kkt, obj, (hipStream_t)stream);
+    return solve_core(p, batch, q0, nullptr, nullptr, line_ref, opts, w, status, iters, kkt, obj, (hipStream_t)stream);
 }
 
-extern "C" int mf_solve_batch(mf_problem *p, int batch, const double *q0, const double *line_ref,
-                              const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt, double *obj,
-                              int device) {
+static int solve_host(mf_problem *p, int batch, const double *q0, const double *qd0, const double *w0,
+                      const double *line_ref, const mf_solver_opts *opts, double *w, int *status, int *iters,
+                      double *kkt, double *obj, int device) {
     if (!p || !q0 || !w || batch < 1) return fail(MF_ERR_ARG, "bad argument");
     int e = ensure_device();
     if (e) return e;
     HIPCHK(hipSetDevice(device));
     const int n = p->C.n, ws = mf_problem_wsize(p);
-    DBuf dq0, dl, dw, dk, dob;
+    DBuf dq0, dqd0, dw0, dl, dw, dk, dob;
     int *dst = nullptr, *dit = nullptr;
     if ((e = h2d(dq0, q0, (size_t)n * batch))) return e;
+    if (qd0 && (e = h2d(dqd0, qd0, (size_t)n * batch))) return e;
+    if (w0 && (e = h2d(dw0, w0, (size_t)ws * batch))) return e;
     if (line_ref && (e = h2d(dl, line_ref, 2 * (size_t)batch))) return e;
     if ((e = dalloc(dw, (size_t)ws * batch)) || (e = dalloc(dk, batch)) || (e = dalloc(dob, batch))) return e;
     HIPCHK(hipMalloc(&dst, sizeof(int) * batch));
     HIPCHK(hipMalloc(&dit, sizeof(int) * batch));
-    e = solve_core(p, batch, dq0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst, dit, dk.p, dob.p, nullptr);
+    e = solve_core(p, batch, dq0.p, dqd0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst, dit, dk.p, dob.p, nullptr);
     if (!e) {
         hipError_t he = hipDeviceSynchronize();
         if (he != hipSuccess) e = fail(MF_ERR_DEVICE, hipGetErrorString(he));
@@ -650,6 +655,25 @@ extern "C" int mf_solve_batch(mf_problem *p, int batch, const double *q0, const 
     (void)hipFree(dst);
     (void)hipFree(dit);
     return e;
+}
+extern "C" int mf_solve_batch(mf_problem *p, int batch, const double *q0, const double *line_ref,
+                              const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt, double *obj,
+                              int device) {
+    return solve_host(p, batch, q0, nullptr, nullptr, line_ref, opts, w, status, iters, kkt, obj, device);
+}
+extern "C" int mf_solve_batch_ws(mf_problem *p, int batch, const double *q0, const double *qd0, const double *w0,
+                                 const double *line_ref, const mf_solver_opts *opts, double *w, int *status,
+                                 int *iters, double *kkt, double *obj, int device) {
+    return solve_host(p, batch, q0, qd0, w0, line_ref, opts, w, status, iters, kkt, obj, device);
+}
+extern "C" int mf_solve_batch_ws_dev(mf_problem *p, int batch, const double *q0, const double *qd0, const double *w0,
+                                     const double *line_ref, const mf_solver_opts *opts, double *w, int *status,
+                                     int *iters, double *kkt, double *obj, void *stream) {
+    if (!p || !q0 || !w || batch < 1) return fail(MF_ERR_ARG, "bad argument");
+    if (w0 && w0 == w) return fail(MF_ERR_ARG, "w0 and w must not alias (w is written while w0 is read)");
+    int e = ensure_device();
+    if (e) return e;
+    return solve_core(p, batch, q0, qd0, w0, line_ref, opts, w, status, iters, kkt, obj, (hipStream_t)stream);
 }
 
 // ====================================================================== node evaluation

@@ -49,6 +49,9 @@ struct IpmArrays {
     double *q0, *lref;
     const double *tau_lo, *tau_hi;  // shared N x n
     ProbState *st;
+    // optional per-solve inputs (device, may be null): per-problem fixed qd_0 (batch x n) and a
+    // warm start in the w layout (batch x wsize)
+    const double *qd0p, *w0;
     int *active;                    // device counter of running problems
 };
 

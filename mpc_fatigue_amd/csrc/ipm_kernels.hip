@@ -385,9 +385,20 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
         A.zqL[b * S.q + e] = (k > 0 && hasb(C.q_lo[j])) ? 1.0 : 0.0;
         A.zqU[b * S.q + e] = (k > 0 && hasb(C.q_hi[j])) ? 1.0 : 0.0;
     }
+    // warm start (w layout [q_0 | (qd_k, F_k, q_{k+1}) for k < N]): q_k, qd_k (k >= 1) and F_k from w0,
+    // pushed into their bounds; q_0, qd_0 stay this problem's
+    const int wst = 2 * NJ + NF, wsz = NJ + N * wst;
+    const double *w0 = A.w0 ? A.w0 + (size_t)b * wsz : nullptr;
+    if (w0) {
+        for (int e = lane + NJ; e < (N + 1) * NJ; e += 64) {
+            const int k = e / NJ, j = e % NJ;
+            q[e] = bound_push(w0[NJ + (k - 1) * wst + NJ + NF + j], C.q_lo[j], C.q_hi[j]);
+        }
+    }
     for (int e = lane; e < N * NJ; e += 64) {
         int k = e / NJ, j = e % NJ;
-        qd[e] = (k == 0) ? C.qd0[j] : bound_push(0.0, C.qd_lo[j], C.qd_hi[j]);
+        const double qd0j = A.qd0p ? A.qd0p[(size_t)b * NJ + j] : C.qd0[j];
+        qd[e] = (k == 0) ? qd0j : bound_push(w0 ? w0[NJ + k * wst + j] : 0.0, C.qd_lo[j], C.qd_hi[j]);
         A.zdL[b * S.u + e] = (k > 0 && hasb(C.qd_lo[j])) ? 1.0 : 0.0;
         A.zdU[b * S.u + e] = (k > 0 && hasb(C.qd_hi[j])) ? 1.0 : 0.0;
         A.vL[b * S.u + e] = hasb(A.tau_lo[e]) ? 1.0 : 0.0;
@@ -395,7 +406,8 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
         A.yc[b * S.u + e] = 0.0;
         A.yd[b * S.u + e] = 0.0;
     }
-    for (int e = lane; e < N * NFA; e += 64) Fv[e] = NF > 0 ? C.F_init : 0.0;
+    for (int e = lane; e < N * NFA; e += 64)
+        Fv[e] = NF > 0 ? (w0 ? w0[NJ + (e / NFA) * wst + NJ + e % NFA] : C.F_init) : 0.0;
     for (int e = lane; e < (int)S.l; e += 64) A.yl[b * S.l + e] = 0.0;
     __syncthreads();
     // slacks from tau at the initial point

@@ -95,6 +95,34 @@ class OCP:
                                              _lib.dptr(kkt), _lib.dptr(obj), device))
         return SolveResult(w, st, it, kkt, obj)
 
+    def solve_ws(self, q0, qd0=None, w0=None, line_ref=None, device: int = 0, **opts) -> SolveResult:
+        """Warm-started solve (mf_solve_batch_ws): per-problem fixed qd_0 and a warm start w0 in
+        the w layout, as the receding-horizon scripts call Solver(x0 = sol, ...)."""
+        q0 = np.ascontiguousarray(np.atleast_2d(np.asarray(q0, float)))
+        B = q0.shape[0]
+        qd = None if qd0 is None else np.ascontiguousarray(np.broadcast_to(np.asarray(qd0, float), (B, self.n)))
+        w0a = None if w0 is None else np.ascontiguousarray(np.broadcast_to(np.asarray(w0, float), (B, self.wsize)))
+        lr = None if line_ref is None else np.ascontiguousarray(np.asarray(line_ref, float).reshape(B, 2))
+        o = default_opts(**opts)
+        w = np.zeros((B, self.wsize))
+        st = np.zeros(B, np.int32)
+        it = np.zeros(B, np.int32)
+        kkt = np.zeros(B)
+        obj = np.zeros(B)
+        _lib.check(_lib.lib().mf_solve_batch_ws(self._h, B, _lib.dptr(q0), None if qd is None else _lib.dptr(qd),
+                                                None if w0a is None else _lib.dptr(w0a),
+                                                None if lr is None else _lib.dptr(lr), C.byref(o), _lib.dptr(w),
+                                                _lib.iptr(st), _lib.iptr(it), _lib.dptr(kkt), _lib.dptr(obj), device))
+        return SolveResult(w, st, it, kkt, obj)
+
+    def solve_ws_dev(self, q0_ptr: int, qd0_ptr, w0_ptr, lref_ptr, batch: int, out: dict, stream: int = 0,
+                     **opts) -> None:
+        """Device-pointer form of solve_ws (qd0_ptr / w0_ptr / lref_ptr may be None)."""
+        o = default_opts(**opts)
+        _lib.check(_lib.lib().mf_solve_batch_ws_dev(self._h, batch, q0_ptr, qd0_ptr, w0_ptr, lref_ptr, C.byref(o),
+                                                    out["w"], out["status"], out["iters"], out["kkt"], out["obj"],
+                                                    stream))
+
     def solve_dev(self, q0_ptr: int, lref_ptr: int | None, batch: int, out: dict, stream: int = 0, **opts) -> None:
         """All pointers are device addresses (e.g. torch tensors' data_ptr())."""
         o = default_opts(**opts)

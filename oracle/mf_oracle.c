@@ -323,6 +323,9 @@ typedef struct {
     int verbose;
     double prox;           /* proximal primal regularisation prox*mu on (q, qd) */
     double F_init;         /* initial guess for every force component */
+    const double *w0;      /* warm start (w layout) or NULL: q_k, qd_k (k >= 1) and F_k from w0, pushed
+                              into their bounds; q_0, qd_0 stay the problem's (IPOPT warm_start_init_point
+                              with x0 = the previous solution, RepeatedMPCwithThermal.py:445-448, 462-487) */
 } mfo_opts;
 
 typedef struct {
@@ -680,6 +683,17 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
         for (int j = 0; j < n; j++)
             S->qd[k * n + j] = (k == 0) ? P->qd0[j] : push_into(0.0, DLO(j), DHI(j));
     for (int k = 0; k < N * nf; k++) S->Fv[k] = O->F_init;
+    if (O->w0) {
+        const int st = 2 * n + nf;
+        for (int k = 0; k < N; k++) {
+            const double *wk = O->w0 + n + (size_t)k * st;
+            for (int j = 0; j < n; j++) {
+                if (k > 0) S->qd[k * n + j] = push_into(wk[j], DLO(j), DHI(j));
+                S->q[(k + 1) * n + j] = push_into(wk[n + nf + j], QLO(j), QHI(j));
+            }
+            for (int a = 0; a < nf; a++) S->Fv[k * nf + a] = wk[n + a];
+        }
+    }
     for (int k = 0; k < N; k++) {
         eval_values(S, S->q + k * n, S->qd + k * n, S->Fv + k * nf, S->tau + k * n, S->line + k * nl);
         for (int j = 0; j < n; j++) S->s[k * n + j] = push_into(S->tau[k * n + j], TLO(k, j), THI(k, j));

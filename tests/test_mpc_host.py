@@ -1,0 +1,35 @@
+"""Host side of the receding-horizon loop: the w-layout split and the
+restart state of mpc_principal.py:357-377, and the oracle's warm start (CPU only)."""
+import numpy as np
+
+from mpc_fatigue_amd import problems as PR
+from mpc_fatigue_amd.mpc import next_initial_state, split_w
+from oracle import oracle as O
+from oracle import pin_np as P
+from oracle.urdf_np import load_urdf_file
+
+
+def test_split_w_layout():
+    n, nf, N = 6, 1, 3
+    w = np.arange(n + N * (2 * n + nf), dtype=float)[None]
+    q, qd, F = split_w(w, n, nf, N)
+    assert q.shape == (1, N + 1, n) and qd.shape == (1, N, n) and F.shape == (1, N, nf)
+    assert q[0, 0, 0] == 0 and qd[0, 0, 0] == n and F[0, 0, 0] == 2 * n and q[0, 1, 0] == 2 * n + nf
+    qN, qdl = next_initial_state(w, n, nf, N)
+    np.testing.assert_array_equal(qN[0], q[0, N])
+    np.testing.assert_array_equal(qdl[0], qd[0, N - 1])
+
+
+
+def test_oracle_warm_start_from_solution():
+    """Warm-starting from a converged solution (multipliers cold) converges to the same point."""
+    N = 10
+    spec = PR.pilz6_bench(N=N)
+    ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
+    q0 = PR.pilz6_batch_q0(1, seed=2)[0]
+    sp = PR.pilz6_bench(N=N, q0=q0, line_ref=P.forward_kinematics(ref, q0, "prbt_link_5")[0][:2])
+    opts = dict(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, F_init=PR.BENCH_F_INIT)
+    w1, r1 = O.solve(ref, sp, **opts)
+    w2, r2 = O.solve(ref, sp, w0=w1, **opts)
+    assert r1.status == 0 and r2.status == 0
+    np.testing.assert_allclose(w2, w1, atol=1e-6)
