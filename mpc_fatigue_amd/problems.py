@@ -108,6 +108,58 @@ def pilz3_working(N: int = 50, T: float = 4.0) -> dict:
     )
 
 
+# ---------------------------------------------------------------- phase-scheduled limits (s.8 a7)
+# The solver takes any per-node torque bounds (tau_lo / tau_hi are N x n); these builders
+# reproduce the reference's phase tables exactly.
+
+# both_robots_torque_limited_2_pilz.py:120-147: limits switched at t = 0.75 s and 1.5 s
+TIME_PHASE_LISTS = ([60, 30, 1000, 300, 300, 50], [10, 100, 50, 500, 1500, 50], [50, 110, 400, 300, 500, 50])
+
+
+def time_phase_limits(N: int, T: float, t1: float = 0.75, t2: float = 1.5, lists=TIME_PHASE_LISTS):
+    """(lo, hi), each N x 6: node i < n1 -> +-list_1, n1 <= i < n2 -> +-list_2, else +-list_3,
+    n1 = int(t1 / h), n2 = int(t2 / h), h = T / N (both_robots_torque_limited_2_pilz.py:120-147)."""
+    h = T / N
+    n1, n2 = int(t1 / h), int(t2 / h)
+    i = np.arange(N)[:, None]
+    lim = np.where(i < n1, np.asarray(lists[0], float), np.where(i < n2, np.asarray(lists[1], float),
+                                                                np.asarray(lists[2], float)))
+    return -lim, lim
+
+
+# Box_Pilz_6DOF.py:287-383: joints 0-2 of the right arm and 0-1 of the left arm follow a
+# three-phase table switched at k = int(N/3), int(2N/3); every other torque row is +-500
+BOX_RIGHT = ([(-200.0, 100.0), (-60.0, 60.0), (-30.0, 40.0)],
+             [(-50.0, 50.0), (-30.0, 10.0), (-20.0, 20.0)],
+             [(-5.0, 5.0), (-5.0, 5.0), (-10.0, 5.0)])
+BOX_LEFT = ([(-600.0, 400.0), (-60.0, 60.0)],
+            [(-50.0, 50.0), (-30.0, 40.0)],
+            [(-5.0, 5.0), (-5.0, 5.0)])
+
+
+def box_phase_limits(N: int, arm: str = "right", constrained: bool = True):
+    """(lo, hi), each N x 6, of one arm of Box_Pilz_6DOF.py (RightConst / LeftConst)."""
+    lo, hi = np.full((N, 6), -500.0), np.full((N, 6), 500.0)
+    if not constrained:
+        return lo, hi
+    table = BOX_RIGHT if arm == "right" else BOX_LEFT
+    for k in range(N):
+        ph = 0 if k < int(N / 3) else (1 if k < int(2 * N / 3) else 2)
+        for j, (a, b) in enumerate(table[ph]):
+            lo[k, j], hi[k, j] = a, b
+    return lo, hi
+
+
+def pilz6_phase(N: int = 100, T: float = 2.0, q0=None, line_ref=(0.1, 0.4), scale: float = 1.0) -> dict:
+    """The C2 force task under the time-phase schedule of both_robots_torque_limited_2_pilz.py
+    (scaled by ``scale``) instead of the exponential envelope: the single-arm instance that runs
+    the a7 bound tables through the solver (the dual-arm OCP itself is s.8f rank 1)."""
+    sp = pilz6_force(N=N, T=T, q0=q0, line_ref=line_ref)
+    lo, hi = time_phase_limits(N, T)
+    sp.update(name="pilz6_phase", tau_lo=lo * scale, tau_hi=hi * scale)
+    return sp
+
+
 def pilz6_batch_q0(batch: int, seed: int = 0, spread: float = 0.05, q0=None) -> np.ndarray:
     """C5 initial states: q0_i = q0 + U(-spread, spread) per joint, numpy default_rng(seed)."""
     base = pilz6_q0() if q0 is None else np.asarray(q0, float)

@@ -158,3 +158,24 @@ def test_solve_pilz6_batch_matches_oracle():
         assert np.abs(F_gpu - F_ref).max() <= 1e-9, (b, np.abs(F_gpu - F_ref).max())
         assert abs(int(res.iters[b]) - R[b].iter) <= 1, (b, res.iters[b], R[b].iter)
         assert abs(res.obj[b] - R[b].obj) <= 1e-9 * abs(R[b].obj)
+
+
+def test_solve_phase_scheduled_matches_oracle():
+    """a7: the C2 force task under the time-phase torque schedule of
+    both_robots_torque_limited_2_pilz.py:120-147 (per-node bounds switched at 0.75 s / 1.5 s)."""
+    N, B = 40, 6
+    base = PR.pilz6_phase(N=N)
+    ocp = OCP(base)
+    ref = load_urdf_file(PR.urdf_path(base["urdf"]))
+    Q0 = PR.pilz6_batch_q0(B, seed=11)
+    LR = np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in Q0])
+    res = ocp.solve(Q0, line_ref=LR, F_init=PR.BENCH_F_INIT, **SOLVE_OPTS)
+    specs = [PR.pilz6_phase(N=N, q0=Q0[b], line_ref=LR[b]) for b in range(B)]
+    W, R = O.solve_batch(ref, specs, F_init=PR.BENCH_F_INIT, **SOLVE_OPTS)
+    for b in range(B):
+        assert R[b].status == 0 and res.status[b] == 0, (b, R[b].status, res.status[b])
+        q_gpu, _, F_gpu = ocp.unpack(res.w[b])
+        q_ref, _, F_ref = ocp.unpack(W[b])
+        assert np.abs(q_gpu - q_ref).max() <= 1e-6, (b, np.abs(q_gpu - q_ref).max())
+        assert np.abs(F_gpu - F_ref).max() <= 1e-6 * max(1.0, np.abs(F_ref).max()), b
+        assert abs(int(res.iters[b]) - R[b].iter) <= 2, (b, res.iters[b], R[b].iter)
