@@ -179,3 +179,21 @@ def test_solve_phase_scheduled_matches_oracle():
         assert np.abs(q_gpu - q_ref).max() <= 1e-6, (b, np.abs(q_gpu - q_ref).max())
         assert np.abs(F_gpu - F_ref).max() <= 1e-6 * max(1.0, np.abs(F_ref).max()), b
         assert abs(int(res.iters[b]) - R[b].iter) <= 2, (b, res.iters[b], R[b].iter)
+
+
+def test_unroll_torques_match_oracle():
+    """solution_io.unroll: per-node torques tau = ID - J^T [F;0] of a solved C2 horizon through the
+    GPU bridge, equal to the oracle's and inside the fatigue envelope."""
+    from mpc_fatigue_amd.solution_io import unroll
+    N = 20
+    ref = load_urdf_file(PR.urdf_path("pilz_robot_6DOF.urdf"))
+    q0 = PR.pilz6_batch_q0(1, seed=4)[0]
+    sp = PR.pilz6_bench(N=N, q0=q0, line_ref=P.forward_kinematics(ref, q0, "prbt_link_5")[0][:2])
+    w, r = O.solve(ref, sp, F_init=PR.BENCH_F_INIT, **SOLVE_OPTS)
+    assert r.status == 0
+    u = unroll(w, sp)
+    for k in range(N):
+        t_ref = (O.inverse_dynamics(ref, u["q"][k], u["qd"][k], np.zeros(6))
+                 - O.jacobian(ref, u["q"][k], "prbt_link_5").T @ np.r_[u["F"][k, 0], 0, 0, 0, 0, 0])
+        np.testing.assert_allclose(u["tau"][k], t_ref, atol=1e-9)
+        assert np.all(u["tau"][k] <= sp["tau_hi"][k] + 1e-6) and np.all(u["tau"][k] >= sp["tau_lo"][k] - 1e-6)
