@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmpcfatigue.so")
+# MF_LIB selects a diagnostic build of the same library (e.g. libmpcfatigue_stamps.so)
+LIB_PATH = os.path.join(HERE, os.environ.get("MF_LIB", "libmpcfatigue.so"))
 MF_MAX_JOINTS = 16
 MF_NKERNELS = 5
 
