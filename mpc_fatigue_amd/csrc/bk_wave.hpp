@@ -36,6 +36,28 @@ __device__ __forceinline__ int wave_sum_i(int x) {
     for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
     return x;
 }
+// reductions over aligned W-lane segments of the wave (W = 64: the whole wave); kernels that
+// give each horizon half a wave reduce with W = 32 and never mix the two halves
+template <int W> __device__ __forceinline__ double hw_sum(double x) {
+#pragma unroll
+    for (int off = W / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, W);
+    return x;
+}
+template <int W> __device__ __forceinline__ double hw_max(double x) {
+#pragma unroll
+    for (int off = W / 2; off > 0; off >>= 1) x = fmax(x, __shfl_xor(x, off, W));
+    return x;
+}
+template <int W> __device__ __forceinline__ double hw_min(double x) {
+#pragma unroll
+    for (int off = W / 2; off > 0; off >>= 1) x = fmin(x, __shfl_xor(x, off, W));
+    return x;
+}
+template <int W> __device__ __forceinline__ int hw_sumi(int x) {
+#pragma unroll
+    for (int off = W / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, W);
+    return x;
+}
 // max |value| with the smallest index among ties (matches a sequential strict-> scan)
 __device__ __forceinline__ void wave_argmax(double &v, int &idx) {
 #pragma unroll

@@ -1,13 +1,17 @@
 // Batched interior-point solve of the fatigue-aware OCP on MI355X (gfx950).
 //
-// One IPM iteration = two launches:
-//   k_eval_node lanes (problem, node, direction v)   forward-over-reverse dual sweep
+// One IPM iteration = six launches (IpmLaunch::iter):
+//   k_eval_node<CLS> lanes (problem, node, direction v)   forward-over-reverse dual sweep
 //               (adj.hpp): tau, line, cost, column v of their Jacobian and of the exact
-//               Lagrangian Hessian; writes the condensed stage Hessian H0
-//   k_ipm_iter  one wavefront per problem             optimality error, barrier update,
-//               inertia-corrected Riccati recursion (Bunch-Kaufman stage blocks in LDS),
-//               step recovery, fraction-to-boundary, l1-merit line search (node_values),
-//               update.  Mirrors oracle/mf_oracle.c mfo_solve statement by statement.
+//               Lagrangian Hessian; one launch per direction class (CLS 0: the q directions,
+//               dual pose; CLS 1: the qd directions, plain-FP64 pose -- its own register
+//               allocation, not the q class's)
+//   k_eval_asm  lanes (problem, node, column)          condensed stage Hessian H0, grad f
+//   k_ipm_pre / k_ipm_kkt / k_ipm_post  one wavefront per problem: optimality error and
+//               barrier update; inertia-corrected Riccati recursion (null-space or
+//               Bunch-Kaufman stage solves in LDS) and step recovery; fraction-to-boundary,
+//               l1-merit line search (node_values) and update.  Together they mirror
+//               oracle/mf_oracle.c mfo_solve statement by statement.
 // Model constants (URDF joint placements, inertias) are staged in LDS per
 // workgroup; per-problem arrays are [problem][node][field] so a wave reading a
 // node's data, and lanes (node, field) writing it, both touch contiguous bytes.
@@ -173,7 +177,7 @@ template <int NJ, int NF, int NV> struct NodeOut {
 // Hessian columns; k_eval_asm adds the Gauss-Newton / barrier terms.  The q-class lanes also
 // write the force columns (d tau / dF_a = -fdir_a . dp_f/dq_v), the line Jacobian, and the
 // node's tau, line residual and cost.
-template <int NJ, int NF, int NL>
+template <int NJ, int NF, int NL, int CLS>
 __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                    OcpConst C, IpmArrays A, int batch, int nb) {
     constexpr int NV = 2 * NJ + NF;
@@ -186,8 +190,8 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     __shared__ double SCs[NPB][NJ][2];  // sin / cos of each node's joint angles
     Ml.load(Mg);
     stage_lds(&F, Fg);
-    const int cls = blockIdx.x < (unsigned)nb ? 0 : 1;
-    const int grp = cls == 0 ? blockIdx.x : blockIdx.x - nb;
+    constexpr int cls = CLS;  // direction class: 0 = q directions, 1 = qd directions (own launch)
+    const int grp = blockIdx.x;
     const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
     const int g = wv * (64 / NJ) + ln / NJ, j0 = ln % NJ, v = cls * NJ + j0;
     const int N = C.N;
@@ -251,14 +255,14 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
         Fw[r] = acc;
     }
     const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
-    if (cls == 0) {
+    if constexpr (cls == 0) {
         NodeIn<NJ, Dual> in{qd, SCs[g], v};
         node_fwd_rev<Dual, Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
     } else {
         NodeIn<NJ, double> in{qd, SCs[g], v};
         node_fwd_rev<double, Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
+        return;
     }
-    if (cls != 0) return;
     // ---- q lanes: force columns of d tau / dw, line Jacobian column; node values (lane 0)
 #pragma unroll
     for (int a = 0; a < NF; a++)
@@ -980,10 +984,15 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
         }
         double glr = 0.0;  // Jl_{k+1} entry of this lane for the next stage
         double sgr = (lane < SG) ? stg[(size_t)(N - 1) * SG + lane] : 0.0;  // stage block, one ahead
+        // block row of Rk holding slot row c (slot rows in control order: qd 0..n-1, F, then the
+        // NL line multipliers)
+        auto brow = [&](int c) { return c < NU ? (c < NJ ? NF + c : c - NJ) : c; };
         wave_lds_sync();
         for (int k = N - 1; k >= 0; k--) {
             // ---- H_k = H0_k (+ regularisation) into LDS; prefetch H0_{k-1}, Jl_k (, J_{k-1})
+            STAMP(18);
             if (lane < SG) Stg[lane] = sgr;
+            STAMP(19);
             if (dreg) {
 #pragma unroll
                 for (int t = 0; t < NJR; t++) {
@@ -1008,23 +1017,32 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
             }
             if (lane < nl * n) Gl[lane] = glr;
             STAMP(7);
+            // ---- Riccati slot stores, then the prefetch loads.  vmcnt retires in order, so the
+            // next stage's wait for its prefetched operands also waits for every store issued
+            // before it: stores issued at the end of a stage (where the slot used to be written)
+            // put a full store round trip on the path of the next stage; issued here, they
+            // complete behind the stage's own work.  P_{k+1}, p_{k+1} (slot k) are in Ps / ps;
+            // stage k+1's Ku, Kl, ku, kl (slot k+1) are still in Rk.
+            double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
+            if (lane < n) wk[NU + NL + lane] = ps[lane];
+            for (int e = lane; e < n * n; e += 64) Gk[(NU + NL) * n + e] = Ps[e];
+            if (k + 1 < N) {
+                double *G1 = G + (size_t)(k + 1) * MB * n, *w1 = wv + (size_t)(k + 1) * MB;
+                for (int e = lane; e < NK * n; e += 64) G1[e] = Rk[brow(e / n) * NRK + e % n];  // Ku (NU x n), Kl (NL x n)
+                if (lane < NK) w1[lane] = Rk[brow(lane) * NRK + n];                             // ku, kl
+            }
             if (k > 0) {
+                // unconditional loads from clamped addresses (a load whose value is selected
+                // against a constant is waited for on the spot)
 #pragma unroll
-                for (int t = 0; t < NHR; t++) {
-                    const int e = lane + 64 * t;
-                    hr[t] = (e < NVV) ? W[(size_t)(k - 1) * NVV + e] : 0.0;
-                }
-                glr = (lane < nl * n) ? Jl[(size_t)k * nl * n + lane] : 0.0;
-                sgr = (lane < SG) ? stg[(size_t)(k - 1) * SG + lane] : 0.0;
+                for (int t = 0; t < NHR; t++) hr[t] = W[(size_t)(k - 1) * NVV + min(lane + 64 * t, NVV - 1)];
+                if constexpr (NL > 0) glr = Jl[(size_t)k * nl * n + min(lane, nl * n - 1)];
+                sgr = stg[(size_t)(k - 1) * SG + min(lane, SG - 1)];
                 if (dreg)
 #pragma unroll
-                    for (int t = 0; t < NJR; t++) {
-                        const int e = lane + 64 * t;
-                        jr[t] = (e < NJV) ? Jt[(size_t)(k - 1) * NJV + e] : 0.0;
-                    }
+                    for (int t = 0; t < NJR; t++) jr[t] = Jt[(size_t)(k - 1) * NJV + min(lane + 64 * t, NJV - 1)];
             }
-            // s = P c + p ; keep P_{k+1}, p_{k+1} for the forward sweep
-            double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
+            // s = P c + p
             const double *ck = Stg + NV;
             if (lane < n) {
                 const int j = lane;
@@ -1032,9 +1050,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
 #pragma unroll
                 for (int i = 0; i < NJ; i++) a += Ps[j * n + i] * ck[i];
                 ss[j] = a;
-                wk[NU + NL + j] = ps[j];
             }
-            for (int e = lane; e < n * n; e += 64) Gk[(NU + NL) * n + e] = Ps[e];
             wave_lds_sync();
             STAMP(11);
             const double *gsk = Stg;
@@ -1138,10 +1154,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
                 if (con)
                     for (int l = 0; l < nl; l++) pnew += Gl[l * n + i] * Rk[(NU + l) * NRK + n];
             }
-            // slot rows in control order (qd 0..n-1, F, then the NL line multipliers)
-            auto brow = [&](int c) { return c < NU ? (c < NJ ? NF + c : c - NJ) : c; };
-            for (int e = lane; e < NK * n; e += 64) Gk[e] = Rk[brow(e / n) * NRK + e % n];  // Ku (NU x n), Kl (NL x n)
-            for (int a = lane; a < NK; a += 64) wk[a] = Rk[brow(a) * NRK + n];              // ku, kl
+            // (Ku, Kl, ku, kl stay in Rk: the next stage stores them, see the slot stores)
             wave_lds_sync();
             for (int e = lane; e < n * n; e += 64) {
                 int i = e / n, j = e % n;
@@ -1184,15 +1197,39 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
     constexpr int FD = 4;
     constexpr int NGL = NL > 0 ? NL * NJ : 1;
     double sr[FD][NSR], glr_f[FD], cr_f[FD];
+    // Every load is unconditional from a clamped address (lanes past the data read a valid
+    // element that is never used): a value selected between two loads, or between a load and a
+    // constant, makes the compiler wait for the load on the spot, which turned the ring into no
+    // prefetch at all.
     auto fetch = [&](int kk, double *srr, double &g, double &cr) {
         const double *Gn = G + (size_t)kk * MB * n, *wn = wv + (size_t)kk * MB;
 #pragma unroll
         for (int t = 0; t < NSR; t++) {
             const int e = lane + 64 * t;
-            srr[t] = (e < SLOT) ? ((e < MB * NJ) ? Gn[e] : wn[e - MB * NJ]) : 0.0;
+            const double *src = (e < MB * NJ) ? Gn + e : wn + min(e - MB * NJ, MB - 1);
+            srr[t] = *src;
         }
-        g = (NL > 0 && lane < NGL && kk + 1 < N) ? Jl[(size_t)(kk + 1) * NGL + lane] : 0.0;
-        cr = (lane < NJ) ? stg[(size_t)kk * SG + NV + lane] : 0.0;  // c_k
+        g = NL > 0 ? Jl[(size_t)min(kk + 1, N - 1) * NGL + min(lane, NGL - 1)] : 0.0;  // used only when con1
+        cr = stg[(size_t)kk * SG + NV + min(lane, NJ - 1)];             // c_k
+    };
+    // A stage's outputs (dq_k | dqd_k | dyc_k | dF_k | dyl_{k+1}) are staged in LDS and stored at
+    // the top of the next stage, before its fetch: the wait at a stage's top then only covers
+    // memory operations issued a stage earlier (vmcnt retires in order; stores issued at the end
+    // of a stage used to put a store round trip on every stage)
+    __shared__ double Fo[3 * NJ + NFA + NLA2];
+    auto flush = [&](int kk) {
+        if (kk == 0) {
+            if (lane < nf) dF[lane] = Fo[3 * n + lane];
+            if (lane < n) dyc[lane] = Fo[2 * n + lane];
+            return;
+        }
+        if (lane < n) {
+            dq[kk * n + lane] = Fo[lane];
+            dqd[kk * n + lane] = Fo[n + lane];
+            dyc[kk * n + lane] = Fo[2 * n + lane];
+        }
+        if (lane < nf) dF[kk * NFA + lane] = Fo[3 * n + lane];
+        if (kk + 1 < N && lane < nl) dyl[(kk + 1) * nl + lane] = Fo[3 * n + NFA + lane];
     };
 #pragma unroll
     for (int r = 0; r < FD; r++)
@@ -1215,15 +1252,16 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
             }
             if (lane < NGL) Gl[lane] = glr_f[r];
             if (lane < NJ) Stg[lane] = cr_f[r];
-            if (k + FD < N) fetch(k + FD, sr[r], glr_f[r], cr_f[r]);
+            if (k > 0) flush(k - 1);
+            fetch(min(k + FD, N - 1), sr[r], glr_f[r], cr_f[r]);  // past the end: slot N-1 again, unused
             wave_lds_sync();
             const double *Gk = Sl, *wk = Sl + MB * NJ;
             if (k == 0) {
-                for (int a = lane; a < nf; a += 64) dF[a] = wk[NJ + a];
+                for (int a = lane; a < nf; a += 64) Fo[3 * n + a] = wk[NJ + a];  // dF_0
                 for (int j = lane; j < n; j += 64) {  // dyc_0 = P_1 dx_1 + p_1 (stage-1 line is masked)
                     double a = wk[NU + NL + j];
                     for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * xs[i];
-                    dyc[j] = a;
+                    Fo[2 * n + j] = a;
                 }
                 wave_lds_sync();
                 continue;
@@ -1233,28 +1271,28 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
                 for (int i = 0; i < n; i++) v += Gk[a * n + i] * xs[i];
                 us[a] = v;
             }
-            for (int j = lane; j < n; j += 64) dq[k * n + j] = xs[j];
+            for (int j = lane; j < n; j += 64) Fo[j] = xs[j];  // dq_k
             wave_lds_sync();
             for (int j = lane; j < n; j += 64) {
-                dqd[k * n + j] = us[j];
+                Fo[n + j] = us[j];  // dqd_k
                 cs[j] = xs[j] + h * us[j] + Stg[j];
             }
-            for (int a = lane; a < nf; a += 64) dF[k * NFA + a] = us[NJ + a];
+            for (int a = lane; a < nf; a += 64) Fo[3 * n + a] = us[NJ + a];  // dF_k
             const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
-            if (k + 1 < N)
-                for (int l = lane; l < nl; l += 64) dyl[(k + 1) * nl + l] = con1 ? us[NU + l] : 0.0;
+            for (int l = lane; l < nl; l += 64) Fo[3 * n + NFA + l] = con1 ? us[NU + l] : 0.0;  // dyl_{k+1}
             wave_lds_sync();
             for (int j = lane; j < n; j += 64) {
                 double a = wk[NU + NL + j];
                 for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * cs[i];
                 if (con1)
                     for (int l = 0; l < nl; l++) a += Gl[l * n + j] * us[NU + l];
-                dyc[k * n + j] = a;
+                Fo[2 * n + j] = a;  // dyc_k
                 xs[j] = cs[j];
             }
             wave_lds_sync();
         }
     }
+    flush(N - 1);
     for (int j = lane; j < n; j += 64) dq[N * n + j] = xs[j];
     __threadfence_block();
     __syncthreads();
@@ -1758,7 +1796,8 @@ struct IpmLaunch {
         long nodes = (long)batch * C.N;
         if (phase == 0) {
             const int nb = (int)((nodes + NPB - 1) / NPB);
-            hipLaunchKernelGGL((k_eval_node<NJ, NF, NL>), dim3(2 * nb), dim3(256), 0, s, M, F, C, A, batch, nb);
+            hipLaunchKernelGGL((k_eval_node<NJ, NF, NL, 0>), dim3(nb), dim3(256), 0, s, M, F, C, A, batch, nb);
+            hipLaunchKernelGGL((k_eval_node<NJ, NF, NL, 1>), dim3(nb), dim3(256), 0, s, M, F, C, A, batch, nb);
         } else if (phase == 1) {
             hipLaunchKernelGGL((k_eval_asm<NJ, NF, NL>), dim3((unsigned)((nodes + NPBA - 1) / NPBA)), dim3(256), 0, s,
                                C, A, batch);

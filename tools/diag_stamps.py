@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from mpc_fatigue_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = os.path.join(ROOT, "mpc_fatigue_amd", "libmpcfatigue_stamps.so")
+_lib.LIB_PATH = os.path.join(ROOT, "mpc_fatigue_amd", os.environ.get("MF_LIB", "libmpcfatigue_stamps.so"))
 from mpc_fatigue_amd import problems as PR  # noqa: E402
 from mpc_fatigue_amd.ocp import OCP  # noqa: E402
 from oracle import pin_np as P  # noqa: E402
@@ -31,10 +31,11 @@ L = _lib.lib()
 buf = (C.c_ulonglong * (32 * B))()
 L.mf_debug_phase_stamps(buf, B)
 a = np.array(buf, dtype=np.float64).reshape(B, 32)
-# KKT sub-phases (per stage, summed): 7 H to LDS, 11 s=Pc+p + slot stores, 12 block assembly,
+# KKT sub-phases (per stage, summed): 18 end of stage to loop top, 19 the wait for the prefetched
+# stage block, 7 H to LDS, 11 s=Pc+p + slot stores, 12 block assembly,
 # 13 Bunch-Kaufman factor, 14 solve, 15 P update; slot 2 keeps the rest of the KKT phase
-cols = [0, 1, 2, 7, 11, 12, 13, 14, 15, 3, 4, 5, 6]
-names = ["opt-err+mu", "barrier", "kkt-other", " kkt:H->LDS", " kkt:s+slot", " kkt:assemble", " kkt:BK-factor",
+cols = [0, 1, 2, 18, 19, 7, 11, 12, 13, 14, 15, 3, 4, 5, 6]
+names = ["opt-err+mu", "barrier", "kkt-other", " kkt:loop-top", " kkt:wait-sgr", " kkt:H->LDS", " kkt:s+slot", " kkt:assemble", " kkt:BK-factor",
          " kkt:BK-solve", " kkt:P-update", "backsub+recover", "ftb+merit0+gdot", "linesearch", "update"]
 a_ = a
 a = a_[:, cols]
