@@ -168,6 +168,10 @@ def main() -> int:
         "avg_launch_ms": per_launch_ms, "launches": dom_launches, "algorithmic_bytes_per_launch": bytes_per_launch,
         "kernel_ms": {k: v[0] for k, v in stats.items()}, "fp64": fp64,
     }
+    if dom == "k_eval_node":
+        roofline["launch_note"] = ("one k_eval_node launch = the solver's phase 0: k_eval_node<..,0> (q directions) "
+                                   "then k_eval_node<..,1> (qd directions) on one stream; rocprofv3 lists the two, "
+                                   "their averages sum to avg_launch_ms")
 
     result = {
         "metric": METRIC, "value": value, "unit": "horizons/s", "n_gpus": world, "steps": args.steps,

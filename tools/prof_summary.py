@@ -11,11 +11,18 @@ def main(db_glob: str, out: str, title: str):
     with open(out, "w") as f:
         f.write(f"# {title}\n\nSource: `{db}` (rocprofv3 --kernel-trace --stats), durations in microseconds.\n\n")
         f.write("| kernel | calls | total us | avg us | % |\n|---|---|---|---|---|\n")
+        ev = []
         for name, calls, tot, avg, pct in rows:
             short = name.split("(")[0].replace("void ", "")
+            if "k_eval_node<" in short:
+                ev.append((calls, tot, avg, pct))
             if len(short) > 80:
                 short = short[:77] + "..."
             f.write(f"| `{short}` | {calls} | {tot:.1f} | {avg:.3f} | {pct:.2f} |\n")
+        if len(ev) == 2:
+            # the solver's phase 0 is one launch of each direction class per iteration
+            f.write(f"| **k_eval_node phase** (both classes) | {ev[0][0]} | {ev[0][1] + ev[1][1]:.1f} | "
+                    f"{ev[0][2] + ev[1][2]:.3f} | {ev[0][3] + ev[1][3]:.2f} |\n")
     print(open(out).read())
 
 
