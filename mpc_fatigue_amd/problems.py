@@ -160,6 +160,102 @@ def pilz6_phase(N: int = 100, T: float = 2.0, q0=None, line_ref=(0.1, 0.4), scal
     return sp
 
 
+# ---------------------------------------------------------------- C3: dual-arm box (s.8 a5, a10, a11)
+# Box_Pilz_6DOF.py: joint limits L176-177, qd in [-1, 0.5] L179-180, m = 30 kg L182,
+# equilibrium tolerance pos_toll = 1e-4 L184, Lbox = 0.2 and the IK targets L94-114.
+BOX_JOINT_LIM = [2.96, 2.53, 2.35, 2.96, 2.96, 3.12]
+_BOX_Q0_FILE = os.path.join(HERE, "data", "box_q0.json")
+
+
+def box_q0() -> np.ndarray:
+    """The dual-arm IK start (Box_Pilz_6DOF.py:123-156), as the reference's committed solution holds it."""
+    with open(_BOX_Q0_FILE) as f:
+        return np.array(json.load(f)["q0"], float)
+
+
+def box_dual(N: int = 50, T: float = 2.0, q0=None, right_const: bool = True, left_const: bool = False,
+             torque_const: bool = True, mass: float = 30.0, Lbox: float = 0.2, qd_lo: float = -1.0,
+             qd_hi: float = 0.5) -> dict:
+    """C3: ``python/2_pilz_6_DOF/Box_Pilz_6DOF.py`` (two Pilz arms holding a box).
+
+    x = [q_L(6), q_R(6)], u = [qd_L(6), qd_R(6), F_L(3), F_R(3)] (L213-262).  Rows per node:
+    force equilibrium F_L + F_R = (0, 0, m g) and moment equilibrium (E1 - E2) x (F_L - F_R) = 0
+    within +-pos_toll (L268-277), torques tau = ID - J^T [F; 0] of both arms in the phase tables
+    (L285-399), end-effector distance |E1 - E2|^2 = L (L279-282), cost
+    100 |(E1 + E2)/2 - p_des|^2 + qd^T qd (L415-416), explicit Euler (L423-436).
+    """
+    h = T / N
+    p1 = np.array([0.2, 0.6, 0.4])
+    p2 = p1 + np.array([Lbox, 0.0, 0.0])
+    lim = np.array(BOX_JOINT_LIM * 2)
+    if torque_const:
+        lo_l, hi_l = box_phase_limits(N, "left", left_const)
+        lo_r, hi_r = box_phase_limits(N, "right", right_const)
+    else:
+        lo_l = lo_r = np.full((N, 6), -INF)
+        hi_l = hi_r = np.full((N, 6), INF)
+    return dict(
+        name="box_dual", family="box", urdf=["pilz_robot_6DOF_first.urdf", "pilz_robot_6DOF_second.urdf"],
+        frame="end_effector", N=N, h=h, n=12, nf=6,
+        q0=list(box_q0() if q0 is None else q0), qd0=[0.0] * 12,
+        qd_lo=[qd_lo] * 12, qd_hi=[qd_hi] * 12, q_lo=list(-lim), q_hi=list(lim),
+        pos_toll=1e-4, box_mg=9.81 * mass, box_L=float((p1 - p2) @ (p1 - p2)), p_des=list((p1 + p2) / 2),
+        w_box=100.0, w_qd=1.0,
+        tau_lo=np.hstack([lo_l, lo_r]), tau_hi=np.hstack([hi_l, hi_r]),
+    )
+
+
+def box_homotopy_tolerances():
+    """Equilibrium-tolerance homotopy of the C3 solve: pos_toll 1 -> 1e-2 -> the
+    reference's 1e-4, each stage warm-started from the previous primal point.  Only the path to the
+    solution changes; the last stage is Box_Pilz_6DOF.py's problem verbatim."""
+    return [1.0, 1e-2, 1e-4]
+
+
+def box_u_init(spec: dict) -> np.ndarray:
+    """Initial control: qd = 0, each arm carries half the box weight (the warm-start force of
+    RepeatedMPCwithThermal.py:148, F0 = [0, 0, m g / 2] per arm)."""
+    mg = spec["box_mg"]
+    return np.r_[np.zeros(12), 0.0, 0.0, mg / 2, 0.0, 0.0, mg / 2]
+
+
+# ---------------------------------------------------------------- thermal fatigue state (s.8 a8)
+# Tmodel_library.py:9-32: Ra = 10, Rh = 2, R_theta = R1 R2 / (R1 + R2) (R1 = 300, R2 = 9), C_theta = 15,
+# T_theta = R_theta C_theta; ktau per joint (L32).  Recursion RepeatedMPCwithThermal.py:371-376:
+#   T_{k+1} = a T_k + R_theta (1 - a) (Ra (tau / ktau)^2 + qd^2 / Rh),  a = exp(-h / T_theta)
+# with T in [0, 80] (L122-123) and T_0 = 20 (L140).
+TH_RA, TH_RH = 10.0, 2.0
+TH_RTHETA = 300.0 * 9.0 / (300.0 + 9.0)
+TH_TTHETA = TH_RTHETA * 15.0
+KTAU14 = (30.0, 40.0, 40.0, 40.0, 40.0, 30.0, 50.0, 30.0, 30.0, 40.0, 40.0, 40.0, 40.0, 50.0)
+
+
+def thermal_coeffs(h: float):
+    """(a, b): T' = a T + b P with a = e^{-h / T_theta}, b = R_theta (1 - a)."""
+    a = float(np.exp(-h / TH_TTHETA))
+    return a, TH_RTHETA * (1.0 - a)
+
+
+def with_thermal(spec: dict, T0=20.0, T_lo: float = 0.0, T_hi: float = 80.0, ktau=None) -> dict:
+    """Adds the motor-winding temperature of every joint as state: x = [q, T], the thermal recursion as
+    dynamics, T in [T_lo, T_hi] for k >= 1.  T0 may be a vector (a receding horizon carries T_N - 0.05,
+    mpc_principal.py:365-374).  ktau defaults to the first n entries of the reference table."""
+    n = len(spec["q0"])
+    a, b = thermal_coeffs(spec["h"])
+    sp = dict(spec)
+    sp.update(name=spec["name"] + "_thermal", thermal=True, th_a=a, th_b=b, Ra=TH_RA, Rh=TH_RH,
+              ktau=list(KTAU14[:n] if ktau is None else ktau), T0=list(np.broadcast_to(np.asarray(T0, float), (n,))),
+              T_lo=T_lo, T_hi=T_hi)
+    return sp
+
+
+def pilz6_thermal(N: int = 100, T0=79.0, q0=None, line_ref=(0.1, 0.4)) -> dict:
+    """Thermal C2 variant (build-defined; parity unpinned by construction): the benchmark force task with
+    the winding temperatures as state, starting hot (T0 = 79 C, one degree under the reference's 80 C
+    limit) so that the temperature bound, not the torque envelope, caps the force."""
+    return with_thermal(pilz6_bench(N=N, q0=q0, line_ref=line_ref), T0=T0)
+
+
 def pilz6_batch_q0(batch: int, seed: int = 0, spread: float = 0.05, q0=None) -> np.ndarray:
     """C5 initial states: q0_i = q0 + U(-spread, spread) per joint, numpy default_rng(seed)."""
     base = pilz6_q0() if q0 is None else np.asarray(q0, float)

@@ -1,0 +1,227 @@
+"""ORACLE (test infrastructure only) — ctypes front-end of the generic stage-structured
+restatement ``mfg_solve`` in ``oracle/mf_ocp.c``.
+
+Converts the problem specs of ``mpc_fatigue_amd.problems`` (plain data) into the
+generic NLP ``x_{k+1} = f(x_k, u_k)``, slack rows ``c_lo <= c_in <= c_hi``,
+state equalities ``c_eq(x_k) = 0``.  Models come from the
+numpy URDF restatement (``oracle/urdf_np.py``), independent of the product parser.
+Nothing in ``mpc_fatigue_amd`` imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import oracle as O
+from .urdf_np import load_urdf_file
+
+MJ = 16
+GX = 32
+MFG_CHAIN, MFG_BOX = 0, 1
+INF = float("inf")
+URDF_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpc_fatigue_amd", "urdf")
+
+# Tmodel_library.py:9-32 (motor-winding thermal model) and RepeatedMPCwithThermal.py:122-140
+TH_RA, TH_RH = 10.0, 2.0
+TH_RTHETA = 300.0 * 9.0 / (300.0 + 9.0)
+TH_TTHETA = TH_RTHETA * 15.0
+KTAU14 = [30.0, 40.0, 40.0, 40.0, 40.0, 30.0, 50.0, 30.0, 30.0, 40.0, 40.0, 40.0, 40.0, 50.0]
+
+
+class GOCP(C.Structure):
+    _fields_ = [
+        ("family", C.c_int), ("N", C.c_int), ("h", C.c_double),
+        ("nx", C.c_int), ("nu", C.c_int), ("ni", C.c_int), ("ne", C.c_int),
+        ("force_from", C.c_int), ("tier1_from", C.c_int), ("tier1_to", C.c_int),
+        ("frame", (C.c_double * 13) * 2), ("nf", C.c_int), ("fdir", C.c_double * 9),
+        ("use_line", C.c_int), ("line_ref", C.c_double * 2),
+        ("wF", C.c_double), ("wqd", C.c_double), ("wtau", C.c_double),
+        ("thermal", C.c_int), ("th_a", C.c_double), ("th_b", C.c_double), ("Ra", C.c_double), ("Rh", C.c_double),
+        ("ktau", C.c_double * MJ), ("wT", C.c_double),
+        ("box_mg", C.c_double), ("box_L", C.c_double), ("box_pdes", C.c_double * 3), ("w_box", C.c_double),
+        ("w_qd", C.c_double),
+        ("x0", C.c_double * GX), ("x_lo", C.c_double * GX), ("x_hi", C.c_double * GX),
+        ("u_lo", C.POINTER(C.c_double)), ("u_hi", C.POINTER(C.c_double)),
+        ("c_lo", C.POINTER(C.c_double)), ("c_hi", C.POINTER(C.c_double)),
+        ("eq_from", C.c_int),
+    ]
+
+
+class GOpts(C.Structure):
+    _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
+                ("mu_init", C.c_double), ("init_zero", C.c_int), ("verbose", C.c_int), ("F_init", C.c_double),
+                ("w0", C.POINTER(C.c_double)), ("bound_relax", C.c_double),
+                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = O.lib()
+        dp = C.POINTER(C.c_double)
+        L.mfg_solve.argtypes = [dp, dp, C.POINTER(GOCP), C.POINTER(GOpts), dp, C.POINTER(O.Result)]
+        L.mfg_solve_batch.argtypes = [dp, dp, C.POINTER(GOCP), C.c_int, C.POINTER(GOpts), dp, C.c_int,
+                                      C.POINTER(O.Result), C.c_int]
+        L.mfg_node_derivs.argtypes = [dp, dp, C.POINTER(GOCP), dp, dp, dp, dp, dp, dp, dp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def models(spec: dict):
+    names = spec["urdf"] if isinstance(spec["urdf"], (list, tuple)) else [spec["urdf"]]
+    return [load_urdf_file(os.path.join(URDF_DIR, u)) for u in names]
+
+
+def thermal_params(N: int, T: float):
+    """a = e^{-h/T_theta}, b = R_theta (1 - a) (RepeatedMPCwithThermal.py:371-376)."""
+    a = float(np.exp(-(T / N) / TH_TTHETA))
+    return a, TH_RTHETA * (1.0 - a)
+
+
+def make(spec: dict):
+    """(GOCP, [blob0, blob1], keep-alive list) for a spec of mpc_fatigue_amd.problems."""
+    ms = models(spec)
+    N = spec["N"]
+    g = GOCP()
+    g.N, g.h = N, spec["h"]
+    keep = []
+    blobs = [O.model_blob(m) for m in ms]
+    if spec.get("family", "chain") == "box":
+        n = 12
+        g.family = MFG_BOX
+        g.nx, g.nu, g.ni, g.ne = n, n + 6, 6 + n, 1
+        g.force_from, g.tier1_from, g.tier1_to = n, 0, 0
+        for a, m in enumerate(ms):
+            g.frame[a][:] = list(O.frame_arr(m, spec["frame"]))
+        g.box_mg, g.box_L = spec["box_mg"], spec["box_L"]
+        g.box_pdes[:] = list(spec["p_des"])
+        g.w_box, g.w_qd = spec["w_box"], spec["w_qd"]
+        x_lo, x_hi = np.asarray(spec["q_lo"], float), np.asarray(spec["q_hi"], float)
+        x0 = np.asarray(spec["q0"], float)
+        tol = spec["pos_toll"]
+        c_lo = np.hstack([np.full((N, 6), -tol), np.asarray(spec["tau_lo"], float)])
+        c_hi = np.hstack([np.full((N, 6), tol), np.asarray(spec["tau_hi"], float)])
+        u_lo = np.hstack([np.tile(np.asarray(spec["qd_lo"], float), (N, 1)), np.full((N, 6), -INF)])
+        u_hi = np.hstack([np.tile(np.asarray(spec["qd_hi"], float), (N, 1)), np.full((N, 6), INF)])
+        u_lo[0, :n] = u_hi[0, :n] = np.asarray(spec["qd0"], float)
+        g.eq_from = 2
+    else:
+        m = ms[0]
+        n, nf = m.nq, spec["nf"]
+        th = bool(spec.get("thermal", False))
+        g.family = MFG_CHAIN
+        g.nx, g.nu, g.ni = (2 * n if th else n), n + nf, n
+        g.ne = 2 if spec["use_line"] else 0
+        g.force_from = n
+        g.tier1_from, g.tier1_to = (n, n + nf) if (nf > 0 and spec["wF"] < 0) else (0, 0)
+        g.frame[0][:] = list(O.frame_arr(m, spec["frame"]))
+        g.nf = nf
+        fd = np.zeros(9)
+        fd[:3 * nf] = np.asarray(spec["fdir"], float).reshape(-1)
+        g.fdir[:] = list(fd)
+        g.use_line = int(spec["use_line"])
+        g.line_ref[:] = list(spec.get("line_ref", [0.0, 0.0]))
+        g.wF, g.wqd, g.wtau = spec["wF"], spec["wqd"], spec["wtau"]
+        x_lo = np.broadcast_to(np.asarray(spec["q_lo"], float), (n,))
+        x_hi = np.broadcast_to(np.asarray(spec["q_hi"], float), (n,))
+        x0 = np.asarray(spec["q0"], float)
+        if th:
+            g.thermal = 1
+            g.th_a, g.th_b = spec["th_a"], spec["th_b"]
+            g.Ra, g.Rh = spec.get("Ra", TH_RA), spec.get("Rh", TH_RH)
+            kt = np.zeros(MJ)
+            kt[:n] = spec["ktau"]
+            g.ktau[:] = list(kt)
+            g.wT = spec.get("wT", 0.0)
+            x_lo = np.r_[x_lo, np.full(n, spec["T_lo"])]
+            x_hi = np.r_[x_hi, np.full(n, spec["T_hi"])]
+            x0 = np.r_[x0, np.broadcast_to(np.asarray(spec["T0"], float), (n,))]
+        c_lo = np.ascontiguousarray(np.broadcast_to(np.asarray(spec["tau_lo"], float), (N, n)))
+        c_hi = np.ascontiguousarray(np.broadcast_to(np.asarray(spec["tau_hi"], float), (N, n)))
+        u_lo = np.hstack([np.tile(np.broadcast_to(np.asarray(spec["qd_lo"], float), (n,)), (N, 1)),
+                          np.full((N, nf), -INF)])
+        u_hi = np.hstack([np.tile(np.broadcast_to(np.asarray(spec["qd_hi"], float), (n,)), (N, 1)),
+                          np.full((N, nf), INF)])
+        qd0 = np.broadcast_to(np.asarray(spec.get("qd0", 0.0), float), (n,))
+        u_lo[0, :n] = u_hi[0, :n] = qd0
+        g.eq_from = 2
+    xa = np.zeros(GX)
+    xa[:len(x0)] = x0
+    g.x0[:] = list(xa)
+    lo = np.full(GX, -INF)
+    hi = np.full(GX, INF)
+    lo[:len(x_lo)] = x_lo
+    hi[:len(x_hi)] = x_hi
+    g.x_lo[:] = list(lo)
+    g.x_hi[:] = list(hi)
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (u_lo, u_hi, c_lo, c_hi)]
+    keep += arrs
+    g.u_lo, g.u_hi, g.c_lo, g.c_hi = (_p(a) for a in arrs)
+    g._keep = keep
+    bl = [np.ascontiguousarray(b) for b in blobs] + [None]
+    return g, bl[:2]
+
+
+def w_size(g: GOCP) -> int:
+    return g.nx + g.N * (g.nu + g.nx)
+
+
+def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, verbose=0, F_init=0.0,
+         w0=None, bound_relax=0.0, u_init=None, max_soc=0):
+    o = GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), F_init, None, bound_relax, None,
+              max_soc)
+    if u_init is not None:
+        o._u_init = np.ascontiguousarray(u_init, dtype=np.float64)
+        o.u_init = _p(o._u_init)
+    if w0 is not None:
+        o._w0 = np.ascontiguousarray(w0, dtype=np.float64)
+        o.w0 = _p(o._w0)
+    return o
+
+
+def solve(spec: dict, **kw):
+    g, (b0, b1) = make(spec)
+    op = opts(**kw)
+    w = np.zeros(w_size(g))
+    r = O.Result()
+    err = lib().mfg_solve(_p(b0), _p(b1), C.byref(g), C.byref(op), _p(w), C.byref(r))
+    if err:
+        raise RuntimeError(f"mfg_solve error {err}")
+    return w, r
+
+
+def solve_batch(specs: list, nthreads: int = 0, **kw):
+    made = [make(s) for s in specs]
+    arr = (GOCP * len(specs))()
+    for i, (g, _) in enumerate(made):
+        arr[i] = g
+    b0, b1 = made[0][1]
+    op = opts(**kw)
+    ws = w_size(made[0][0])
+    w = np.zeros((len(specs), ws))
+    res = (O.Result * len(specs))()
+    err = lib().mfg_solve_batch(_p(b0), _p(b1), arr, len(specs), C.byref(op), _p(w), ws, res, nthreads)
+    if err:
+        raise RuntimeError(f"mfg_solve_batch error {err}")
+    return w, list(res)
+
+
+def node_derivs(spec: dict, xu, yi, ye, lam):
+    """(vals, jac, H): vals = [l, c_in, c_eq, f]; jac rows = same outputs w.r.t. [x|u]; H = Hessian of
+    l + yi.c_in + ye.c_eq + lam.f."""
+    g, (b0, b1) = make(spec)
+    nv = g.nx + g.nu
+    no = 1 + g.ni + g.ne + g.nx
+    arrs = [np.ascontiguousarray(a, float) for a in (xu, yi, ye if g.ne else [0.0], lam)]
+    vals, jac, H = np.zeros(no), np.zeros(no * nv), np.zeros(nv * nv)
+    lib().mfg_node_derivs(_p(b0), _p(b1), C.byref(g), *[_p(a) for a in arrs], _p(vals), _p(jac), _p(H))
+    return vals, jac.reshape(no, nv), H.reshape(nv, nv)

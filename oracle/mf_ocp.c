@@ -1,0 +1,1111 @@
+/*
+ * ORACLE — test infrastructure only.  Generic stage-structured CPU restatement
+ * (plain C99, FP64) of the reference's OCP solves.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only
+ * as the checker / timed CPU baseline; libmpcfatigue.so never links it.
+ *
+ * NLP (one horizon; every reference transcription has this shape):
+ *   w = [x_0 | (u_k, x_{k+1}) for k < N]          (force_optimization_pilz_6DOF.py:103-172,
+ *                                                  Box_Pilz_6DOF.py:213-436,
+ *                                                  RepeatedMPCwithThermal.py:183-402)
+ *   min  sum_k l(x_k, u_k)
+ *   s.t. x_{k+1} = f(x_k, u_k)                    explicit Euler (+ thermal recursion)
+ *        c_lo[k] <= c_in(x_k, u_k) <= c_hi[k]     torques, equilibrium rows (slack rows)
+ *        c_eq(x_k) = 0,  eq_from <= k < N         state-only equalities (line, distance)
+ *        x_lo <= x_k <= x_hi (k >= 1), u_lo[k] <= u_k <= u_hi[k]  (lo == hi: fixed)
+ * Families (node functions, hyper-dual so every derivative is exact):
+ *   MFG_CHAIN  one serial arm: Pilz 3/6-DOF (C1, C2), optionally with the motor-winding
+ *              thermal state T (Tmodel_library.py:9-41, RepeatedMPCwithThermal.py:371-376)
+ *   MFG_BOX    two arms holding a box (C3, Box_Pilz_6DOF.py:219-456)
+ * Solver: the IPOPT-style primal-dual interior point of DESIGN.md section 4 (the same
+ * iteration mf_oracle.c runs for the Pilz family), with a block-tridiagonal KKT over
+ * shooting nodes factorised block by block with Bunch-Kaufman (inertia = sum over
+ * blocks, Sylvester) -- an algorithm independent of the device's Riccati recursion.
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "hd_kin.h"
+
+#define GX 32              /* max state size */
+#define GU 32              /* max control size */
+#define GV (GX + GU)       /* max node variables */
+#define GI 48              /* max slack (inequality) rows */
+#define GE 8               /* max equality rows */
+#define GB (2 * GX + GU + GE)
+
+enum { MFG_CHAIN = 0, MFG_BOX = 1 };
+
+typedef struct {
+    int family;
+    int N;
+    double h;
+    int nx, nu, ni, ne;
+    int force_from;                 /* u index of the first force component (F_init / warm start) */
+    int tier1_from, tier1_to;       /* u range regularised first (concave cost block), empty if equal */
+    /* MFG_CHAIN */
+    double frame[2][13];            /* frame records (parent, R row-major, t) of chain 0 / 1 */
+    int nf;
+    double fdir[9];
+    int use_line;
+    double line_ref[2];
+    double wF, wqd, wtau;
+    int thermal;
+    double th_a, th_b, Ra, Rh;      /* T' = th_a T + th_b (Ra (tau/ktau)^2 + qd^2 / Rh) */
+    double ktau[MJ];
+    double wT;                      /* optional thermal stage cost wT |T|^2 (0 in the reference) */
+    /* MFG_BOX */
+    double box_mg, box_L, box_pdes[3], w_box, w_qd;
+    /* bounds / data */
+    double x0[GX];
+    double x_lo[GX], x_hi[GX];      /* states k >= 1 */
+    const double *u_lo, *u_hi;      /* N x nu */
+    const double *c_lo, *c_hi;      /* N x ni */
+    int eq_from;
+} mfg_ocp;
+
+typedef struct {
+    double tol, constr_viol_tol;
+    int max_iter;
+    double mu_init;
+    int init_zero;                  /* 1: IPOPT's x0 = 0 for every free variable; 0: hold x_0 */
+    int verbose;
+    double F_init;
+    const double *w0;               /* warm start (w layout) or NULL */
+    double bound_relax;             /* IPOPT bound_relax_factor (0 = off) */
+    const double *u_init;           /* initial control (nu) for every node, or NULL (0 / F_init) */
+    int max_soc;                    /* IPOPT max_soc (second-order corrections per iteration; 0 = off) */
+} mfg_opts;
+
+typedef struct {
+    int status, iter;
+    double kkt, cviol, obj, mu;
+    int n_ls_fail, n_inertia_fix;
+} mfg_result;
+
+typedef struct {
+    mfo_model M[2];
+    mfo_frame F[2];
+} models_t;
+
+static int hasb(double b) { return isfinite(b); }
+
+/* ------------------------------------------------------------------ node functions */
+static void chain_tau(const mfo_model *M, const mfo_frame *Fr, const hd *q, const hd *qd, const hd *Fw, int with_force,
+                      hd *tau, hd *pf) {
+    kin_t Kn;
+    hd zero[MJ], R[9];
+    kinematics(M, q, &Kn);
+    for (int i = 0; i < M->n; i++) zero[i] = K(0);
+    rnea(M, &Kn, qd, zero, tau);
+    frame_pose(&Kn, Fr, pf, R);
+    if (with_force) sub_external(M, &Kn, Fr, pf, Fw, tau);
+}
+
+/* l, c_in (ni), c_eq (ne), f (nx) at the node variables xu = [x | u] */
+static void node_hd(const mfg_ocp *P, const models_t *MM, const hd *xu, hd *l, hd *ci, hd *ce, hd *f) {
+    const int nx = P->nx;
+    const hd *u = xu + nx;
+    if (P->family == MFG_CHAIN) {
+        const int n = MM->M[0].n, nf = P->nf;
+        const hd *q = xu, *qd = u, *F = u + n;
+        hd tau[MJ], pf[3], Fw[3] = {K(0), K(0), K(0)};
+        for (int a = 0; a < nf; a++)
+            for (int r = 0; r < 3; r++) Fw[r] = add(Fw[r], muls(F[a], P->fdir[3 * a + r]));
+        chain_tau(&MM->M[0], &MM->F[0], q, qd, Fw, nf > 0, tau, pf);
+        hd c = K(0);
+        for (int a = 0; a < nf; a++) c = add(c, muls(mul(F[a], F[a]), P->wF));
+        for (int j = 0; j < n; j++) {
+            c = add(c, muls(mul(qd[j], qd[j]), P->wqd));
+            c = add(c, muls(mul(tau[j], tau[j]), P->wtau));
+            ci[j] = tau[j];
+            f[j] = add(q[j], muls(qd[j], P->h));
+        }
+        if (P->use_line)
+            for (int i = 0; i < 2; i++) ce[i] = sub(pf[i], K(P->line_ref[i]));
+        if (P->thermal) {
+            const hd *T = xu + n;
+            for (int j = 0; j < n; j++) {
+                hd ia = muls(tau[j], 1.0 / P->ktau[j]);
+                hd pl = add(muls(mul(ia, ia), P->Ra), muls(mul(qd[j], qd[j]), 1.0 / P->Rh));
+                f[n + j] = add(muls(T[j], P->th_a), muls(pl, P->th_b));
+                if (P->wT != 0.0) c = add(c, muls(mul(T[j], T[j]), P->wT));
+            }
+        }
+        *l = c;
+        return;
+    }
+    /* MFG_BOX: x = [qL(6) qR(6)], u = [qdL(6) qdR(6) FL(3) FR(3)] */
+    const int na = MM->M[0].n;
+    const hd *qL = xu, *qR = xu + na, *qdL = u, *qdR = u + na, *FL = u + 2 * na, *FR = u + 2 * na + 3;
+    hd tL[MJ], tR[MJ], E1[3], E2[3];
+    chain_tau(&MM->M[0], &MM->F[0], qL, qdL, FL, 1, tL, E1);
+    chain_tau(&MM->M[1], &MM->F[1], qR, qdR, FR, 1, tR, E2);
+    hd d[3], dF[3], mom[3];
+    for (int r = 0; r < 3; r++) { d[r] = sub(E1[r], E2[r]); dF[r] = sub(FL[r], FR[r]); }
+    cross3(mom, d, dF);   /* cross(E1-E2, F_L) + cross(E2-E1, F_R)  (Box_Pilz_6DOF.py:274) */
+    ci[0] = sub(add(FL[2], FR[2]), K(P->box_mg));   /* Box_Pilz_6DOF.py:269 */
+    ci[1] = add(FL[0], FR[0]);
+    ci[2] = add(FL[1], FR[1]);
+    for (int r = 0; r < 3; r++) ci[3 + r] = mom[r];
+    for (int j = 0; j < na; j++) { ci[6 + j] = tL[j]; ci[6 + na + j] = tR[j]; }
+    ce[0] = sub(dot3(d, d), K(P->box_L));          /* Box_Pilz_6DOF.py:280 */
+    hd c = K(0);
+    for (int r = 0; r < 3; r++) {                   /* 100 |p_box - p_des|^2 + qd^T qd (L415-416) */
+        hd e = sub(muls(add(E1[r], E2[r]), 0.5), K(P->box_pdes[r]));
+        c = add(c, muls(mul(e, e), P->w_box));
+    }
+    for (int j = 0; j < 2 * na; j++) {
+        c = add(c, muls(mul(u[j], u[j]), P->w_qd));
+        f[j] = add(xu[j], muls(u[j], P->h));
+    }
+    *l = c;
+}
+
+/* ------------------------------------------------------------------ workspace */
+typedef struct {
+    const mfg_ocp *P;
+    const models_t *MM;
+    int N, nx, nu, nv, ni, ne, mb;
+    /* per-variable masks (after relaxation) */
+    double *ulo, *uhi, *clo, *chi;   /* N x nu, N x ni */
+    double xlo[GX], xhi[GX];
+    unsigned char *ufix;             /* N x nu */
+    /* iterate */
+    double *x, *u, *s, *lam, *ye, *yi;
+    double *zxL, *zxU, *zuL, *zuU, *vL, *vU;
+    /* trial */
+    double *tx, *tu, *ts;
+    /* eval cache (per node) */
+    double *l, *gl, *ci, *Ji, *ce, *Je, *f, *Af, *Bf, *W;
+    /* step */
+    double *dx, *du, *ds, *dlam, *dye, *dyi, *dzxL, *dzxU, *dzuL, *dzuU, *dvL, *dvU;
+    /* barrier */
+    double *Sx, *gx, *Su, *gu, *Ss, *gs;
+    /* kkt */
+    double *wv, *G, *Dsave;
+    int *perm, *piv;
+    double dw, dc, d1;               /* regularisation of the current factorisation */
+    /* constraint residuals: current point, trial point, second-order correction */
+    double *rdyn, *rin, *req, *trdyn, *trin, *treq, *sdyn, *sin_, *seq;
+    double *bk;                      /* saved direction (second-order corrections) */
+} ws_t;
+
+static double *dal(size_t n) { return (double *)calloc(n ? n : 1, sizeof(double)); }
+
+#define EQ_ON(S, k) ((k) >= (S)->P->eq_from && (k) < (S)->N)
+#define CACT(S, k, r) (hasb((S)->clo[(k) * (S)->ni + (r)]) || hasb((S)->chi[(k) * (S)->ni + (r)]))
+/* free variable a (0..nv) of node k */
+static int vfree(const ws_t *S, int k, int a) {
+    if (a < S->nx) return k > 0;
+    return !S->ufix[k * S->nu + a - S->nx];
+}
+
+static void eval_values(const ws_t *S, int k, const double *x, const double *u, double *l, double *ci, double *ce,
+                        double *f) {
+    hd xu[GV], hl, hci[GI], hce[GE], hf[GX];
+    for (int a = 0; a < S->nx; a++) xu[a] = K(x[a]);
+    for (int a = 0; a < S->nu; a++) xu[S->nx + a] = K(u[a]);
+    node_hd(S->P, S->MM, xu, &hl, hci, hce, hf);
+    *l = hl.a;
+    for (int r = 0; r < S->ni; r++) ci[r] = hci[r].a;
+    for (int e = 0; e < S->ne; e++) ce[e] = hce[e].a;
+    for (int j = 0; j < S->nx; j++) f[j] = hf[j].a;
+}
+
+static void eval_derivs(ws_t *S, int k) {
+    const int nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne;
+    const double *x = S->x + k * nx, *u = S->u + k * nu;
+    double *gl = S->gl + k * nv, *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + k * ne * nx;
+    double *Af = S->Af + k * nx * nx, *Bf = S->Bf + k * nx * nu, *W = S->W + (size_t)k * nv * nv;
+    const double *lam = S->lam + k * nx, *yi = S->yi + k * ni, *ye = S->ye + k * ne;
+    const int eqon = EQ_ON(S, k);
+    eval_values(S, k, x, u, S->l + k, S->ci + k * ni, S->ce + k * ne, S->f + k * nx);
+    memset(gl, 0, sizeof(double) * nv);
+    memset(Ji, 0, sizeof(double) * ni * nv);
+    memset(Je, 0, sizeof(double) * ne * nx);
+    memset(Af, 0, sizeof(double) * nx * nx);
+    memset(Bf, 0, sizeof(double) * nx * nu);
+    memset(W, 0, sizeof(double) * nv * nv);
+    int fv[GV], nfv = 0;
+    for (int a = 0; a < nv; a++)
+        if (vfree(S, k, a)) fv[nfv++] = a;
+    double xu[GV];
+    memcpy(xu, x, nx * sizeof(double));
+    memcpy(xu + nx, u, nu * sizeof(double));
+    for (int ia = 0; ia < nfv; ia++)
+        for (int ib = ia; ib < nfv; ib++) {
+            const int a = fv[ia], b = fv[ib];
+            hd hx[GV], hl, hci[GI], hce[GE], hf[GX];
+            for (int i = 0; i < nv; i++) hx[i] = K(xu[i]);
+            hx[a].b = 1.0;
+            hx[b].c = 1.0;
+            node_hd(S->P, S->MM, hx, &hl, hci, hce, hf);
+            double h2 = hl.d;
+            for (int r = 0; r < ni; r++) h2 += yi[r] * hci[r].d;
+            if (eqon)
+                for (int e = 0; e < ne; e++) h2 += ye[e] * hce[e].d;
+            for (int j = 0; j < nx; j++) h2 += lam[j] * hf[j].d;
+            W[a * nv + b] = W[b * nv + a] = h2;
+            if (a == b) {
+                gl[a] = hl.b;
+                for (int r = 0; r < ni; r++) Ji[r * nv + a] = hci[r].b;
+                if (a < nx) {
+                    for (int e = 0; e < ne; e++) Je[e * nx + a] = hce[e].b;
+                    for (int j = 0; j < nx; j++) Af[j * nx + a] = hf[j].b;
+                } else {
+                    for (int j = 0; j < nx; j++) Bf[j * nu + a - nx] = hf[j].b;
+                }
+            }
+        }
+}
+
+static double push_into(double x, double lo, double hi) {
+    const double k1 = 1e-2, k2 = 1e-2;
+    int hl = hasb(lo), hh = hasb(hi);
+    if (hl && hh) {
+        double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
+        double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
+        x = fmax(x, lo + pl);
+        x = fmin(x, hi - pu);
+    } else if (hl) {
+        x = fmax(x, lo + k1 * fmax(1.0, fabs(lo)));
+    } else if (hh) {
+        x = fmin(x, hi - k1 * fmax(1.0, fabs(hi)));
+    }
+    return x;
+}
+
+/* barrier objective and l1 constraint violation at (x, u, s); optionally the residual vectors */
+static void merit_parts(const ws_t *S, const double *x, const double *u, const double *s, double mu, double *phi,
+                        double *theta, int *ok, double *rdyn, double *rin, double *req) {
+    const int N = S->N, nx = S->nx, nu = S->nu, ni = S->ni, ne = S->ne;
+    double fsum = 0, bar = 0, th = 0;
+    int good = 1;
+#ifdef _OPENMP
+#pragma omp parallel for reduction(+ : fsum, th) schedule(static)
+#endif
+    for (int k = 0; k < N; k++) {
+        double l, ci[GI], ce[GE], f[GX];
+        eval_values(S, k, x + k * nx, u + k * nu, &l, ci, ce, f);
+        fsum += l;
+        for (int j = 0; j < nx; j++) {
+            const double r = f[j] - x[(k + 1) * nx + j];
+            th += fabs(r);
+            if (rdyn) rdyn[k * nx + j] = r;
+        }
+        for (int q = 0; q < ni; q++) {
+            const double r = CACT(S, k, q) ? ci[q] - s[k * ni + q] : 0.0;
+            th += fabs(r);
+            if (rin) rin[k * ni + q] = r;
+        }
+        const int eqon = EQ_ON(S, k);
+        for (int e = 0; e < ne; e++) {
+            const double r = eqon ? ce[e] : 0.0;
+            th += fabs(r);
+            if (req) req[k * ne + e] = r;
+        }
+    }
+#define BAR(v, lo, hi)                                              \
+    do {                                                            \
+        if (hasb(lo)) { if ((v) - (lo) <= 0) good = 0; else bar -= log((v) - (lo)); } \
+        if (hasb(hi)) { if ((hi) - (v) <= 0) good = 0; else bar -= log((hi) - (v)); } \
+    } while (0)
+    for (int k = 1; k <= N; k++)
+        for (int j = 0; j < nx; j++) BAR(x[k * nx + j], S->xlo[j], S->xhi[j]);
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < nu; j++)
+            if (!S->ufix[k * nu + j]) BAR(u[k * nu + j], S->ulo[k * nu + j], S->uhi[k * nu + j]);
+    for (int k = 0; k < N; k++)
+        for (int r = 0; r < ni; r++) BAR(s[k * ni + r], S->clo[k * ni + r], S->chi[k * ni + r]);
+#undef BAR
+    *phi = fsum + mu * bar;
+    *theta = th;
+    *ok = good;
+}
+
+static void residuals_cached(const ws_t *S, double *rdyn, double *rin, double *req) {
+    const int N = S->N, nx = S->nx, ni = S->ni, ne = S->ne;
+    for (int k = 0; k < N; k++) {
+        for (int j = 0; j < nx; j++) rdyn[k * nx + j] = S->f[k * nx + j] - S->x[(k + 1) * nx + j];
+        for (int q = 0; q < ni; q++) rin[k * ni + q] = CACT(S, k, q) ? S->ci[k * ni + q] - S->s[k * ni + q] : 0.0;
+        for (int e = 0; e < ne; e++) req[k * ne + e] = EQ_ON(S, k) ? S->ce[k * ne + e] : 0.0;
+    }
+}
+
+/* Block-tridiagonal KKT over shooting nodes, block k < N: [lam_{k-1} (nx) | x_k (nx) | u_k (nu) | ye_k (ne)],
+ * block N: [lam_{N-1} | x_N].  lam_k's row lives in block k+1 and couples to block k through
+ * C_k = [0 | A_k | B_k | 0].  Slack rows are condensed: D_s = (Sigma_s + dw) / (1 + dc (Sigma_s + dw)).
+ * Factorises block by block (Bunch-Kaufman, D_{k+1}[lam,lam] -= C_k D_k^-1 C_k^T) and stores the factors.
+ * Returns 0 if the inertia is (n_primal, n_dual, 0), 1 if it is wrong, 2 on a zero pivot.          */
+static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
+    const mfg_ocp *P = S->P;
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne, mb = S->mb;
+    const int ol = 0, ox = nx, ou = 2 * nx, oe = 2 * nx + nu;
+    int npos_t = 0, nneg_t = 0, nzero_t = 0;
+    S->dw = dw; S->dc = dc; S->d1 = d1;
+    for (int k = 0; k <= N; k++) {
+        const int m = (k < N) ? mb : 2 * nx;
+        double *Dm = S->Dsave + (size_t)k * mb * mb;
+        memset(Dm, 0, sizeof(double) * mb * mb);
+#define D_(i, j) Dm[(i) * m + (j)]
+        for (int j = 0; j < nx; j++) {
+            if (k > 0) {
+                D_(ol + j, ol + j) = -dc;
+                D_(ol + j, ox + j) = D_(ox + j, ol + j) = -1.0;
+            } else {
+                D_(ol + j, ol + j) = -1.0; /* lam_{-1}: dummy */
+            }
+        }
+        if (k < N) {
+            const double *W = S->W + (size_t)k * nv * nv, *Ji = S->Ji + (size_t)k * ni * nv;
+            const double *Je = S->Je + k * ne * nx;
+            double Dd[GI];
+            for (int q = 0; q < ni; q++) {
+                const double sg = S->Ss[k * ni + q] + dw;
+                Dd[q] = CACT(S, k, q) ? sg / (1.0 + dc * sg) : 0.0;
+            }
+            for (int a = 0; a < nv; a++)
+                for (int b = 0; b < nv; b++) {
+                    double v = W[a * nv + b];
+                    for (int q = 0; q < ni; q++) v += Ji[q * nv + a] * Dd[q] * Ji[q * nv + b];
+                    D_(ox + a, ox + b) = v;
+                }
+            for (int a = 0; a < nv; a++) {
+                double dd = dw;
+                if (a < nx) dd += S->Sx[k * nx + a];
+                else {
+                    dd += S->Su[k * nu + a - nx];
+                    if (a - nx >= P->tier1_from && a - nx < P->tier1_to) dd += d1;
+                }
+                D_(ox + a, ox + a) += dd;
+            }
+            const int eqon = EQ_ON(S, k);
+            for (int e = 0; e < ne; e++) {
+                if (eqon) {
+                    for (int j = 0; j < nx; j++) D_(oe + e, ox + j) = D_(ox + j, oe + e) = Je[e * nx + j];
+                    D_(oe + e, oe + e) = -dc;
+                } else {
+                    D_(oe + e, oe + e) = -1.0;
+                }
+            }
+            for (int a = 0; a < nv; a++)
+                if (!vfree(S, k, a)) {
+                    for (int v = 0; v < m; v++) { D_(ox + a, v) = 0; D_(v, ox + a) = 0; }
+                    D_(ox + a, ox + a) = 1.0;
+                }
+        } else {
+            for (int j = 0; j < nx; j++) D_(ox + j, ox + j) = S->Sx[N * nx + j] + dw;
+        }
+        if (k > 0) {
+            const double *Gp = S->G + (size_t)(k - 1) * mb * nx;
+            const double *A = S->Af + (k - 1) * nx * nx, *B = S->Bf + (k - 1) * nx * nu;
+            for (int c = 0; c < nx; c++)
+                for (int c2 = 0; c2 < nx; c2++) {
+                    double a = 0;
+                    for (int j = 0; j < nx; j++)
+                        if (vfree(S, k - 1, j)) a += A[c * nx + j] * Gp[(ox + j) * nx + c2];
+                    for (int j = 0; j < nu; j++)
+                        if (vfree(S, k - 1, nx + j)) a += B[c * nu + j] * Gp[(ou + j) * nx + c2];
+                    D_(ol + c, ol + c2) -= a;
+                }
+        }
+#undef D_
+        int np, nn, nz;
+        bk_factor(Dm, m, S->perm + k * mb, S->piv + k * mb, &np, &nn, &nz);
+        npos_t += np; nneg_t += nn; nzero_t += nz;
+        if (nz) return 2;
+        if (k < N) {
+            const double *A = S->Af + k * nx * nx, *B = S->Bf + k * nx * nu;
+            double *Gk = S->G + (size_t)k * mb * nx;
+            for (int c = 0; c < nx; c++) {
+                double e[BKMAX];
+                memset(e, 0, sizeof e);
+                for (int j = 0; j < nx; j++)
+                    if (vfree(S, k, j)) e[ox + j] = A[c * nx + j];
+                for (int j = 0; j < nu; j++)
+                    if (vfree(S, k, nx + j)) e[ou + j] = B[c * nu + j];
+                bk_solve(Dm, m, S->perm + k * mb, S->piv + k * mb, e);
+                for (int i = 0; i < m; i++) Gk[i * nx + c] = e[i];
+            }
+        }
+    }
+    const int want_pos = N * nv + nx, want_neg = (N + 1) * nx + N * ne;
+    return (npos_t == want_pos && nneg_t == want_neg) ? 0 : 1;
+}
+
+/* Newton direction with the stored factorisation for constraint residuals (rdyn, rin, req): the
+ * primal-dual step (dx, du, dlam, dye), the slack-row steps (dyi, ds) and the bound-multiplier steps. */
+static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *rin, const double *req) {
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne, mb = S->mb;
+    const int ol = 0, ox = nx, ou = 2 * nx, oe = 2 * nx + nu;
+    const double dw = S->dw, dc = S->dc;
+    for (int k = 0; k <= N; k++) {
+        const int m = (k < N) ? mb : 2 * nx;
+        double *r = S->wv + (size_t)k * mb;
+        memset(r, 0, sizeof(double) * mb);
+        if (k > 0)
+            for (int j = 0; j < nx; j++) r[ol + j] = -rdyn[(k - 1) * nx + j];
+        if (k < N) {
+            const double *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + k * ne * nx;
+            double Dd[GI], rdd[GI];
+            for (int q = 0; q < ni; q++) {
+                const int i = k * ni + q;
+                if (CACT(S, k, q)) {
+                    const double sg = S->Ss[i] + dw;
+                    Dd[q] = sg / (1.0 + dc * sg);
+                    rdd[q] = rin[i] + (S->gs[i] - S->yi[i]) / sg;
+                } else { Dd[q] = 0; rdd[q] = 0; }
+            }
+            const int eqon = EQ_ON(S, k);
+            for (int e = 0; e < ne; e++) r[oe + e] = eqon ? -req[k * ne + e] : 0.0;
+            for (int a = 0; a < nv; a++) {
+                if (!vfree(S, k, a)) { r[ox + a] = 0; continue; }
+                double g = S->gl[k * nv + a];
+                for (int q = 0; q < ni; q++) g += Ji[q * nv + a] * (S->yi[k * ni + q] + Dd[q] * rdd[q]);
+                if (a < nx) {
+                    g += S->gx[k * nx + a] - (k > 0 ? S->lam[(k - 1) * nx + a] : 0.0);
+                    for (int jj = 0; jj < nx; jj++) g += S->Af[(k * nx + jj) * nx + a] * S->lam[k * nx + jj];
+                    if (eqon)
+                        for (int e = 0; e < ne; e++) g += Je[e * nx + a] * S->ye[k * ne + e];
+                } else {
+                    g += S->gu[k * nu + a - nx];
+                    for (int jj = 0; jj < nx; jj++) g += S->Bf[(k * nx + jj) * nu + a - nx] * S->lam[k * nx + jj];
+                }
+                r[ox + a] = -g;
+            }
+        } else {
+            for (int j = 0; j < nx; j++) r[ox + j] = -(S->gx[N * nx + j] - S->lam[(N - 1) * nx + j]);
+        }
+        if (k > 0) {
+            const double *wp = S->wv + (size_t)(k - 1) * mb;
+            const double *A = S->Af + (k - 1) * nx * nx, *B = S->Bf + (k - 1) * nx * nu;
+            for (int c = 0; c < nx; c++) {
+                double a = 0;
+                for (int j = 0; j < nx; j++)
+                    if (vfree(S, k - 1, j)) a += A[c * nx + j] * wp[ox + j];
+                for (int j = 0; j < nu; j++)
+                    if (vfree(S, k - 1, nx + j)) a += B[c * nu + j] * wp[ou + j];
+                r[ol + c] -= a;
+            }
+        }
+        bk_solve(S->Dsave + (size_t)k * mb * mb, m, S->perm + k * mb, S->piv + k * mb, r);
+    }
+    /* back substitution: y_N = w_N, y_k = w_k - G_k y_{k+1}[lam_k] */
+    {
+        double ynext[BKMAX], y[BKMAX];
+        const double *yN = S->wv + (size_t)N * mb;
+        for (int j = 0; j < nx; j++) { S->dx[N * nx + j] = yN[ox + j]; S->dlam[(N - 1) * nx + j] = yN[ol + j]; }
+        memcpy(ynext, yN, sizeof(double) * 2 * nx);
+        for (int k = N - 1; k >= 0; k--) {
+            const double *wk = S->wv + (size_t)k * mb, *Gk = S->G + (size_t)k * mb * nx;
+            for (int i = 0; i < mb; i++) {
+                double a = wk[i];
+                for (int c = 0; c < nx; c++) a -= Gk[i * nx + c] * ynext[ol + c];
+                y[i] = a;
+            }
+            for (int j = 0; j < nx; j++) {
+                S->dx[k * nx + j] = (k > 0) ? y[ox + j] : 0.0;
+                if (k > 0) S->dlam[(k - 1) * nx + j] = y[ol + j];
+            }
+            for (int j = 0; j < nu; j++) S->du[k * nu + j] = S->ufix[k * nu + j] ? 0.0 : y[ou + j];
+            for (int e = 0; e < ne; e++) S->dye[k * ne + e] = EQ_ON(S, k) ? y[oe + e] : 0.0;
+            memcpy(ynext, y, sizeof(double) * mb);
+        }
+    }
+    for (int k = 0; k < N; k++) {
+        const double *Ji = S->Ji + (size_t)k * ni * nv;
+        for (int q = 0; q < ni; q++) {
+            const int i = k * ni + q;
+            if (!CACT(S, k, q)) { S->dyi[i] = 0; S->ds[i] = 0; continue; }
+            double jd = 0;
+            for (int a = 0; a < nx; a++) jd += Ji[q * nv + a] * S->dx[k * nx + a];
+            for (int a = 0; a < nu; a++) jd += Ji[q * nv + nx + a] * S->du[k * nu + a];
+            const double sg = S->Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
+            const double rs = S->gs[i] - S->yi[i];
+            S->dyi[i] = Dd * (jd + rin[i] + rs / sg);
+            S->ds[i] = (S->dyi[i] - rs) / sg;
+        }
+    }
+#define DZ(dzl, dzu, zl, zu, v, dv, lo, hi)                                              \
+    do {                                                                                 \
+        dzl = dzu = 0;                                                                   \
+        if (hasb(lo)) dzl = mu / ((v) - (lo)) - (zl) - (zl) / ((v) - (lo)) * (dv);       \
+        if (hasb(hi)) dzu = mu / ((hi) - (v)) - (zu) + (zu) / ((hi) - (v)) * (dv);       \
+    } while (0)
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            if (k == 0) { S->dzxL[i] = S->dzxU[i] = 0; continue; }
+            DZ(S->dzxL[i], S->dzxU[i], S->zxL[i], S->zxU[i], S->x[i], S->dx[i], S->xlo[j], S->xhi[j]);
+        }
+    for (int i = 0; i < N * nu; i++) {
+        if (S->ufix[i]) { S->dzuL[i] = S->dzuU[i] = 0; continue; }
+        DZ(S->dzuL[i], S->dzuU[i], S->zuL[i], S->zuU[i], S->u[i], S->du[i], S->ulo[i], S->uhi[i]);
+    }
+    for (int i = 0; i < N * ni; i++)
+        DZ(S->dvL[i], S->dvU[i], S->vL[i], S->vU[i], S->s[i], S->ds[i], S->clo[i], S->chi[i]);
+#undef DZ
+}
+
+/* fraction to the boundary of the current direction */
+#define FTB(v, dv, lo, hi, zl, dzl, zu, dzu)                                                      \
+    do {                                                                                          \
+        if (hasb(lo)) { if ((dv) < 0) ap = fmin(ap, -tau_fb * ((v) - (lo)) / (dv));                \
+                        if ((dzl) < 0) az = fmin(az, -tau_fb * (zl) / (dzl)); }                   \
+        if (hasb(hi)) { if ((dv) > 0) ap = fmin(ap, tau_fb * ((hi) - (v)) / (dv));                 \
+                        if ((dzu) < 0) az = fmin(az, -tau_fb * (zu) / (dzu)); }                   \
+    } while (0)
+static void ftb(const ws_t *S, double tau_fb, double *ap_out, double *az_out) {
+    const int N = S->N, nx = S->nx, nu = S->nu, ni = S->ni;
+    double ap = 1.0, az = 1.0;
+    for (int k = 1; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            FTB(S->x[i], S->dx[i], S->xlo[j], S->xhi[j], S->zxL[i], S->dzxL[i], S->zxU[i], S->dzxU[i]);
+        }
+    for (int i = 0; i < N * nu; i++)
+        if (!S->ufix[i]) FTB(S->u[i], S->du[i], S->ulo[i], S->uhi[i], S->zuL[i], S->dzuL[i], S->zuU[i], S->dzuU[i]);
+    for (int i = 0; i < N * ni; i++)
+        FTB(S->s[i], S->ds[i], S->clo[i], S->chi[i], S->vL[i], S->dvL[i], S->vU[i], S->dvU[i]);
+    *ap_out = ap;
+    *az_out = az;
+}
+static void ftb_report(const ws_t *S, double tau_fb) {
+    const int N = S->N, nx = S->nx, nu = S->nu, ni = S->ni;
+    double ap = 1.0, az = 1.0;
+    for (int k = 1; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            FTB(S->x[i], S->dx[i], S->xlo[j], S->xhi[j], S->zxL[i], S->dzxL[i], S->zxU[i], S->dzxU[i]);
+        }
+    for (int i = 0; i < N * nu; i++)
+        if (!S->ufix[i]) FTB(S->u[i], S->du[i], S->ulo[i], S->uhi[i], S->zuL[i], S->dzuL[i], S->zuU[i], S->dzuU[i]);
+    const double apx = ap;
+    for (int i = 0; i < N * ni; i++) {
+        const double a0 = ap;
+        FTB(S->s[i], S->ds[i], S->clo[i], S->chi[i], S->vL[i], S->dvL[i], S->vU[i], S->dvU[i]);
+        if (ap < a0)
+            fprintf(stderr, "      ftb s k %d row %d s %.4e ds %.4e c %.4e [%g, %g] -> %.3e\n", i / ni, i % ni, S->s[i],
+                    S->ds[i], S->ci[i], S->clo[i], S->chi[i], ap);
+    }
+    fprintf(stderr, "   ftb x/u %.3e all %.3e\n", apx, ap);
+}
+#undef FTB
+
+/* directional derivative of the barrier objective and the curvature term of the penalty update */
+static void direction_model(const ws_t *S, double *gdot_out, double *pHp_out) {
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni;
+    double gdot = 0, pHp = 0;
+    for (int k = 0; k < N; k++) {
+        const double *W = S->W + (size_t)k * nv * nv;
+        double d[GV];
+        for (int a = 0; a < nx; a++) d[a] = S->dx[k * nx + a];
+        for (int a = 0; a < nu; a++) d[nx + a] = S->du[k * nu + a];
+        for (int a = 0; a < nv; a++) {
+            gdot += S->gl[k * nv + a] * d[a];
+            for (int b = 0; b < nv; b++) pHp += d[a] * W[a * nv + b] * d[b];
+        }
+        for (int a = 0; a < nu; a++) {
+            const int i = k * nu + a;
+            gdot += S->gu[i] * S->du[i];
+            pHp += S->Su[i] * S->du[i] * S->du[i];
+        }
+        for (int q = 0; q < ni; q++) {
+            const int i = k * ni + q;
+            gdot += S->gs[i] * S->ds[i];
+            pHp += S->Ss[i] * S->ds[i] * S->ds[i];
+        }
+    }
+    for (int i = nx; i < (N + 1) * nx; i++) {
+        gdot += S->gx[i] * S->dx[i];
+        pHp += S->Sx[i] * S->dx[i] * S->dx[i];
+    }
+    *gdot_out = gdot;
+    *pHp_out = pHp;
+}
+
+static void trial_point(ws_t *S, double alpha) {
+    const size_t NX1 = (size_t)(S->N + 1) * S->nx, NU = (size_t)S->N * S->nu, NI = (size_t)S->N * S->ni;
+    for (size_t i = 0; i < NX1; i++) S->tx[i] = S->x[i] + alpha * S->dx[i];
+    for (size_t i = 0; i < NU; i++) S->tu[i] = S->u[i] + alpha * S->du[i];
+    for (size_t i = 0; i < NI; i++) S->ts[i] = S->s[i] + alpha * S->ds[i];
+}
+
+/* the direction arrays, in a fixed order, for save / restore around second-order corrections */
+static int dir_arrays(ws_t *S, double ***arr, size_t *len) {
+    const size_t NX1 = (size_t)(S->N + 1) * S->nx, NXN = (size_t)S->N * S->nx, NU = (size_t)S->N * S->nu,
+                 NI = (size_t)S->N * S->ni, NE = (size_t)S->N * S->ne;
+    double **a[] = {&S->dx, &S->du, &S->ds, &S->dlam, &S->dye, &S->dyi, &S->dzxL, &S->dzxU, &S->dzuL, &S->dzuU,
+                    &S->dvL, &S->dvU};
+    const size_t l[] = {NX1, NU, NI, NXN, NE, NI, NX1, NX1, NU, NU, NI, NI};
+    for (int i = 0; i < 12; i++) { arr[i] = a[i]; len[i] = l[i]; }
+    return 12;
+}
+static void save_direction(ws_t *S) {
+    double **arr[12];
+    size_t len[12], off = 0;
+    const int na = dir_arrays(S, arr, len);
+    for (int i = 0; i < na; i++) { memcpy(S->bk + off, *arr[i], len[i] * sizeof(double)); off += len[i]; }
+}
+static void restore_direction(ws_t *S) {
+    double **arr[12];
+    size_t len[12], off = 0;
+    const int na = dir_arrays(S, arr, len);
+    for (int i = 0; i < na; i++) { memcpy(*arr[i], S->bk + off, len[i] * sizeof(double)); off += len[i]; }
+}
+
+int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const mfg_opts *O, double *w_out,
+              mfg_result *res) {
+    models_t MM;
+    memset(&MM, 0, sizeof MM);
+    if (mfo_model_from_blob(blob0, &MM.M[0])) return -1;
+    frame_from_arr(P->frame[0], &MM.F[0]);
+    if (P->family == MFG_BOX) {
+        if (!blob1 || mfo_model_from_blob(blob1, &MM.M[1])) return -1;
+        frame_from_arr(P->frame[1], &MM.F[1]);
+    }
+    const int N = P->N, nx = P->nx, nu = P->nu, nv = nx + nu, ni = P->ni, ne = P->ne;
+    const int mb = 2 * nx + nu + ne;
+    if (N < 1 || nx > GX || nu > GU || ni > GI || ne > GE || mb > BKMAX) return -2;
+    ws_t SS, *S = &SS;
+    memset(S, 0, sizeof *S);
+    S->P = P; S->MM = &MM;
+    S->N = N; S->nx = nx; S->nu = nu; S->nv = nv; S->ni = ni; S->ne = ne; S->mb = mb;
+    const double h_unused = P->h; (void)h_unused;
+
+    /* ---- bounds (IPOPT bound_relax_factor on every non-fixed bound) ---- */
+    const double br = O->bound_relax;
+#define RELAX_LO(b) ((b) - br * fmax(1.0, fabs(b)))
+#define RELAX_HI(b) ((b) + br * fmax(1.0, fabs(b)))
+    S->ulo = dal((size_t)N * nu); S->uhi = dal((size_t)N * nu); S->ufix = (unsigned char *)calloc((size_t)N * nu, 1);
+    S->clo = dal((size_t)N * ni); S->chi = dal((size_t)N * ni);
+    for (int j = 0; j < nx; j++) {
+        S->xlo[j] = hasb(P->x_lo[j]) ? RELAX_LO(P->x_lo[j]) : P->x_lo[j];
+        S->xhi[j] = hasb(P->x_hi[j]) ? RELAX_HI(P->x_hi[j]) : P->x_hi[j];
+    }
+    for (int i = 0; i < N * nu; i++) {
+        double lo = P->u_lo[i], hi = P->u_hi[i];
+        if (hasb(lo) && lo == hi) { S->ufix[i] = 1; S->ulo[i] = S->uhi[i] = lo; continue; }
+        S->ulo[i] = hasb(lo) ? RELAX_LO(lo) : lo;
+        S->uhi[i] = hasb(hi) ? RELAX_HI(hi) : hi;
+    }
+    for (int i = 0; i < N * ni; i++) {
+        double lo = P->c_lo[i], hi = P->c_hi[i];
+        S->clo[i] = hasb(lo) ? RELAX_LO(lo) : lo;
+        S->chi[i] = hasb(hi) ? RELAX_HI(hi) : hi;
+    }
+#undef RELAX_LO
+#undef RELAX_HI
+
+    /* ---- allocation ---- */
+    const size_t NX1 = (size_t)(N + 1) * nx, NU = (size_t)N * nu, NI = (size_t)N * ni, NE = (size_t)N * ne;
+    S->x = dal(NX1); S->u = dal(NU); S->s = dal(NI); S->lam = dal((size_t)N * nx); S->ye = dal(NE); S->yi = dal(NI);
+    S->zxL = dal(NX1); S->zxU = dal(NX1); S->zuL = dal(NU); S->zuU = dal(NU); S->vL = dal(NI); S->vU = dal(NI);
+    S->tx = dal(NX1); S->tu = dal(NU); S->ts = dal(NI);
+    S->l = dal(N); S->gl = dal((size_t)N * nv); S->ci = dal(NI); S->Ji = dal(NI * nv); S->ce = dal(NE);
+    S->Je = dal(NE * nx); S->f = dal((size_t)N * nx); S->Af = dal((size_t)N * nx * nx); S->Bf = dal((size_t)N * nx * nu);
+    S->W = dal((size_t)N * nv * nv);
+    S->dx = dal(NX1); S->du = dal(NU); S->ds = dal(NI); S->dlam = dal((size_t)N * nx); S->dye = dal(NE);
+    S->dyi = dal(NI); S->dzxL = dal(NX1); S->dzxU = dal(NX1); S->dzuL = dal(NU); S->dzuU = dal(NU);
+    S->dvL = dal(NI); S->dvU = dal(NI);
+    S->Sx = dal(NX1); S->gx = dal(NX1); S->Su = dal(NU); S->gu = dal(NU); S->Ss = dal(NI); S->gs = dal(NI);
+    S->wv = dal((size_t)(N + 1) * mb); S->G = dal((size_t)(N + 1) * mb * nx);
+    S->Dsave = dal((size_t)(N + 1) * mb * mb);
+    S->rdyn = dal((size_t)N * nx); S->rin = dal(NI); S->req = dal(NE);
+    S->trdyn = dal((size_t)N * nx); S->trin = dal(NI); S->treq = dal(NE);
+    S->sdyn = dal((size_t)N * nx); S->sin_ = dal(NI); S->seq = dal(NE);
+    S->bk = dal(3 * NX1 + 3 * NU + 4 * NI + (size_t)N * nx + NE);
+    S->perm = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
+    S->piv = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
+
+    /* ---- initial point (IPOPT: x0 = 0 or the held state, bound_push / bound_frac = 1e-2) ---- */
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            double v = (k == 0 || !O->init_zero) ? P->x0[j] : 0.0;
+            S->x[k * nx + j] = (k == 0) ? P->x0[j] : push_into(v, S->xlo[j], S->xhi[j]);
+        }
+    for (int k = 0; k < N; k++)
+        for (int j = 0; j < nu; j++) {
+            const int i = k * nu + j;
+            double v = O->u_init ? O->u_init[j] : ((j >= P->force_from) ? O->F_init : 0.0);
+            S->u[i] = S->ufix[i] ? S->ulo[i] : push_into(v, S->ulo[i], S->uhi[i]);
+        }
+    if (O->w0) {
+        const int st = nu + nx;
+        for (int k = 0; k < N; k++) {
+            const double *wk = O->w0 + nx + (size_t)k * st;
+            for (int j = 0; j < nu; j++) {
+                const int i = k * nu + j;
+                if (!S->ufix[i]) S->u[i] = push_into(wk[j], S->ulo[i], S->uhi[i]);
+            }
+            for (int j = 0; j < nx; j++) S->x[(k + 1) * nx + j] = push_into(wk[nu + j], S->xlo[j], S->xhi[j]);
+        }
+    }
+    for (int k = 0; k < N; k++) {
+        double l, ci[GI], ce[GE], f[GX];
+        eval_values(S, k, S->x + k * nx, S->u + k * nu, &l, ci, ce, f);
+        for (int r = 0; r < ni; r++) S->s[k * ni + r] = push_into(ci[r], S->clo[k * ni + r], S->chi[k * ni + r]);
+    }
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            S->zxL[k * nx + j] = (k > 0 && hasb(S->xlo[j])) ? 1.0 : 0.0;
+            S->zxU[k * nx + j] = (k > 0 && hasb(S->xhi[j])) ? 1.0 : 0.0;
+        }
+    for (int i = 0; i < N * nu; i++) {
+        S->zuL[i] = (!S->ufix[i] && hasb(S->ulo[i])) ? 1.0 : 0.0;
+        S->zuU[i] = (!S->ufix[i] && hasb(S->uhi[i])) ? 1.0 : 0.0;
+    }
+    for (int i = 0; i < N * ni; i++) {
+        S->vL[i] = hasb(S->clo[i]) ? 1.0 : 0.0;
+        S->vU[i] = hasb(S->chi[i]) ? 1.0 : 0.0;
+    }
+
+    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
+    const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
+    double mu = O->mu_init, nu_pen = 0.0, reg_last = 0.0;
+    int reg_tier = 0, status = 1, it = 0, n_ls_fail = 0, n_ic = 0, consecutive_fail = 0, n_soc = 0;
+    double E0 = INFINITY, cviol = INFINITY;
+    const int has_tier1 = P->tier1_to > P->tier1_from;
+
+    for (it = 0; it <= O->max_iter; it++) {
+        /* ---- node derivatives ---- */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+        for (int k = 0; k < N; k++) eval_derivs(S, k);
+
+        /* ---- optimality error (IPOPT E_0 with s_max scaling) ---- */
+        double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sum_mult = 0, sum_bmult = 0;
+        int n_mult = 0, n_bmult = 0;
+#define COMP(z, gap)                                                            \
+    do {                                                                        \
+        double c_ = (z) * (gap);                                                \
+        cinf0 = fmax(cinf0, fabs(c_)); cinfm = fmax(cinfm, fabs(c_ - mu));      \
+        sum_bmult += (z); n_bmult++;                                            \
+    } while (0)
+        for (int k = 1; k <= N; k++)
+            for (int j = 0; j < nx; j++) {
+                const int i = k * nx + j;
+                double r = -S->lam[(k - 1) * nx + j];
+                if (k < N) {
+                    r += S->gl[k * nv + j];
+                    for (int jj = 0; jj < nx; jj++) r += S->Af[(k * nx + jj) * nx + j] * S->lam[k * nx + jj];
+                    for (int q = 0; q < ni; q++) r += S->Ji[((size_t)k * ni + q) * nv + j] * S->yi[k * ni + q];
+                    if (EQ_ON(S, k))
+                        for (int e = 0; e < ne; e++) r += S->Je[(k * ne + e) * nx + j] * S->ye[k * ne + e];
+                }
+                r += -S->zxL[i] + S->zxU[i];
+                dinf = fmax(dinf, fabs(r));
+                if (hasb(S->xlo[j])) COMP(S->zxL[i], S->x[i] - S->xlo[j]);
+                if (hasb(S->xhi[j])) COMP(S->zxU[i], S->xhi[j] - S->x[i]);
+            }
+        for (int k = 0; k < N; k++) {
+            for (int j = 0; j < nu; j++) {
+                const int i = k * nu + j;
+                if (S->ufix[i]) continue;
+                double r = S->gl[k * nv + nx + j];
+                for (int jj = 0; jj < nx; jj++) r += S->Bf[(k * nx + jj) * nu + j] * S->lam[k * nx + jj];
+                for (int q = 0; q < ni; q++) r += S->Ji[((size_t)k * ni + q) * nv + nx + j] * S->yi[k * ni + q];
+                r += -S->zuL[i] + S->zuU[i];
+                dinf = fmax(dinf, fabs(r));
+                if (hasb(S->ulo[i])) COMP(S->zuL[i], S->u[i] - S->ulo[i]);
+                if (hasb(S->uhi[i])) COMP(S->zuU[i], S->uhi[i] - S->u[i]);
+            }
+            for (int q = 0; q < ni; q++) {
+                const int i = k * ni + q;
+                if (!CACT(S, k, q)) continue;
+                double r = -S->yi[i] - S->vL[i] + S->vU[i];
+                dinf = fmax(dinf, fabs(r));
+                if (hasb(S->clo[i])) COMP(S->vL[i], S->s[i] - S->clo[i]);
+                if (hasb(S->chi[i])) COMP(S->vU[i], S->chi[i] - S->s[i]);
+                pinf = fmax(pinf, fabs(S->ci[i] - S->s[i]));
+                sum_mult += fabs(S->yi[i]); n_mult++;
+            }
+            for (int j = 0; j < nx; j++) {
+                pinf = fmax(pinf, fabs(S->f[k * nx + j] - S->x[(k + 1) * nx + j]));
+                sum_mult += fabs(S->lam[k * nx + j]); n_mult++;
+            }
+            if (EQ_ON(S, k))
+                for (int e = 0; e < ne; e++) {
+                    pinf = fmax(pinf, fabs(S->ce[k * ne + e]));
+                    sum_mult += fabs(S->ye[k * ne + e]); n_mult++;
+                }
+        }
+#undef COMP
+        const double sd = fmax(s_max, (sum_mult + sum_bmult) / fmax(1, n_mult + n_bmult)) / s_max;
+        const double sc = fmax(s_max, sum_bmult / fmax(1, n_bmult)) / s_max;
+        E0 = fmax(fmax(dinf / sd, pinf), cinf0 / sc);
+        cviol = pinf;
+        double Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
+        if (O->verbose) {
+            double fo = 0;
+            for (int k = 0; k < N; k++) fo += S->l[k];
+            fprintf(stderr, "it %3d f %+.10e dinf %.2e pinf %.2e compl %.2e mu %.1e nu %.2e\n", it, fo, dinf, pinf,
+                    cinf0, mu, nu_pen);
+        }
+        if (E0 <= O->tol && cviol <= O->constr_viol_tol) { status = 0; break; }
+        if (it == O->max_iter) { status = 1; break; }
+        while (Emu <= kappa_eps * mu && mu > O->tol / 10.0) {
+            double mnew = fmax(O->tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
+            if (mnew >= mu) break;
+            mu = mnew;
+            cinfm = 0;
+            for (int k = 1; k <= N; k++)
+                for (int j = 0; j < nx; j++) {
+                    const int i = k * nx + j;
+                    if (hasb(S->xlo[j])) cinfm = fmax(cinfm, fabs(S->zxL[i] * (S->x[i] - S->xlo[j]) - mu));
+                    if (hasb(S->xhi[j])) cinfm = fmax(cinfm, fabs(S->zxU[i] * (S->xhi[j] - S->x[i]) - mu));
+                }
+            for (int i = 0; i < N * nu; i++) {
+                if (S->ufix[i]) continue;
+                if (hasb(S->ulo[i])) cinfm = fmax(cinfm, fabs(S->zuL[i] * (S->u[i] - S->ulo[i]) - mu));
+                if (hasb(S->uhi[i])) cinfm = fmax(cinfm, fabs(S->zuU[i] * (S->uhi[i] - S->u[i]) - mu));
+            }
+            for (int i = 0; i < N * ni; i++) {
+                if (hasb(S->clo[i])) cinfm = fmax(cinfm, fabs(S->vL[i] * (S->s[i] - S->clo[i]) - mu));
+                if (hasb(S->chi[i])) cinfm = fmax(cinfm, fabs(S->vU[i] * (S->chi[i] - S->s[i]) - mu));
+            }
+            Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
+        }
+        const double tau_fb = fmax(tau_min, 1.0 - mu);
+
+        /* ---- barrier Sigma and gradients ---- */
+#define SIGG(Sg, gg, z_l, z_u, v, lo, hi)                                                  \
+    do {                                                                                   \
+        Sg = 0; gg = 0;                                                                    \
+        if (hasb(lo)) { Sg += (z_l) / ((v) - (lo)); gg -= mu / ((v) - (lo)); }             \
+        if (hasb(hi)) { Sg += (z_u) / ((hi) - (v)); gg += mu / ((hi) - (v)); }             \
+    } while (0)
+        for (int k = 0; k <= N; k++)
+            for (int j = 0; j < nx; j++) {
+                const int i = k * nx + j;
+                if (k == 0) { S->Sx[i] = S->gx[i] = 0; continue; }
+                SIGG(S->Sx[i], S->gx[i], S->zxL[i], S->zxU[i], S->x[i], S->xlo[j], S->xhi[j]);
+            }
+        for (int i = 0; i < N * nu; i++) {
+            if (S->ufix[i]) { S->Su[i] = S->gu[i] = 0; continue; }
+            SIGG(S->Su[i], S->gu[i], S->zuL[i], S->zuU[i], S->u[i], S->ulo[i], S->uhi[i]);
+        }
+        for (int i = 0; i < N * ni; i++) SIGG(S->Ss[i], S->gs[i], S->vL[i], S->vU[i], S->s[i], S->clo[i], S->chi[i]);
+#undef SIGG
+
+        /* ---- inertia-corrected block factorisation ---- */
+        double dw = 0.0, dc = 0.0, d1 = 0.0;
+        int tier = reg_tier, step_no = 0, factor_ok = 0, tries;
+        double reg = (reg_tier == 0) ? 0.0 : reg_last / 3.0;
+        if (reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
+        if (tier == 1) d1 = reg; else if (tier == 2) dw = reg;
+        for (tries = 0; tries < 60; tries++) {
+            const int fr = kkt_factor(S, dw, dc, d1);
+            if (fr == 0) { factor_ok = 1; break; }
+            if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
+            n_ic++;
+            step_no++;
+            if (tier == 0) {
+                tier = has_tier1 ? 1 : 2;
+                reg = 1e-4;
+            } else if (step_no == 1 && reg_tier == tier && reg < reg_last) {
+                reg = reg_last;
+            } else {
+                reg *= 8.0;
+                if (tier == 1 && reg > 1e6) { tier = 2; reg = 1e-4; }
+            }
+            if (reg > 1e40) break;
+            d1 = (tier == 1) ? reg : 0.0;
+            dw = (tier == 2) ? reg : 0.0;
+        }
+        if (!factor_ok) { status = 3; break; }
+        reg_tier = tier;
+        reg_last = reg;
+        if (O->verbose > 1) fprintf(stderr, "   d1 %.2e dw %.2e dc %.2e tries %d\n", d1, dw, dc, tries);
+
+        /* ---- Newton direction for the residuals of the current point ---- */
+        residuals_cached(S, S->rdyn, S->rin, S->req);
+        kkt_direction(S, mu, S->rdyn, S->rin, S->req);
+        double ap, az;
+        ftb(S, tau_fb, &ap, &az);
+        if (O->verbose > 2) ftb_report(S, tau_fb);
+
+        /* ---- l1-merit backtracking line search with second-order corrections ---- */
+        double phi0, th0;
+        int ok0;
+        merit_parts(S, S->x, S->u, S->s, mu, &phi0, &th0, &ok0, NULL, NULL, NULL);
+        double gdot = 0, pHp = 0;
+        direction_model(S, &gdot, &pHp);
+        if (th0 > 1e-300) {
+            double nreq = (gdot + 0.5 * fmax(pHp, 0.0)) / ((1.0 - rho) * th0);
+            if (nu_pen < nreq) nu_pen = nreq + 1.0;
+        }
+        const double Dphi = gdot - nu_pen * th0, m0 = phi0 + nu_pen * th0;
+        const double slack_m = 10.0 * 2.220446049250313e-16 * fabs(m0);
+        double alpha = ap;
+        int accepted = 0, soc_used = 0;
+        for (int ls = 0; ls < 40; ls++) {
+            double ph, th;
+            int okk;
+            trial_point(S, alpha);
+            merit_parts(S, S->tx, S->tu, S->ts, mu, &ph, &th, &okk, S->trdyn, S->trin, S->treq);
+            const double mt = ph + nu_pen * th;
+            if (okk && isfinite(mt) && mt - m0 <= eta * alpha * fmin(Dphi, 0.0) + slack_m) { accepted = 1; break; }
+            /* IPOPT A-5.5..A-5.9: second-order corrections after the first trial step when it raised the
+             * infeasibility: c_soc = alpha c(x) + c(x_trial), same factorisation, up to O->max_soc tries */
+            if (ls == 0 && O->max_soc > 0 && (!okk || th >= th0)) {
+                double th_old = th, a_soc = alpha;
+                for (size_t i = 0; i < (size_t)N * nx; i++) S->sdyn[i] = alpha * S->rdyn[i] + S->trdyn[i];
+                for (size_t i = 0; i < (size_t)N * ni; i++) S->sin_[i] = alpha * S->rin[i] + S->trin[i];
+                for (size_t i = 0; i < (size_t)N * ne; i++) S->seq[i] = alpha * S->req[i] + S->treq[i];
+                for (int p = 0; p < O->max_soc; p++) {
+                    save_direction(S);
+                    kkt_direction(S, mu, S->sdyn, S->sin_, S->seq);
+                    double aps, azs;
+                    ftb(S, tau_fb, &aps, &azs);
+                    trial_point(S, aps);
+                    double phs, ths;
+                    int oks;
+                    merit_parts(S, S->tx, S->tu, S->ts, mu, &phs, &ths, &oks, S->trdyn, S->trin, S->treq);
+                    const double ms = phs + nu_pen * ths;
+                    if (O->verbose > 1)
+                        fprintf(stderr, "      soc %d a %.3e th %.3e (th0 %.3e) m %.10e (m0 %.10e)\n", p, aps, ths, th0, ms, m0);
+                    if (oks && isfinite(ms) && ms - m0 <= eta * a_soc * fmin(Dphi, 0.0) + slack_m) {
+                        accepted = 1; soc_used = 1; alpha = aps; az = azs;
+                        break;
+                    }
+                    restore_direction(S);
+                    if (!oks || ths > 0.99 * th_old) break;
+                    th_old = ths;
+                    for (size_t i = 0; i < (size_t)N * nx; i++) S->sdyn[i] = aps * S->sdyn[i] + S->trdyn[i];
+                    for (size_t i = 0; i < (size_t)N * ni; i++) S->sin_[i] = aps * S->sin_[i] + S->trin[i];
+                    for (size_t i = 0; i < (size_t)N * ne; i++) S->seq[i] = aps * S->seq[i] + S->treq[i];
+                }
+                if (accepted) break;
+            }
+            alpha *= 0.5;
+        }
+        if (O->verbose) fprintf(stderr, "   ap %.3e az %.3e alpha %.3e acc %d soc %d\n", ap, az, alpha, accepted, soc_used);
+        if (!accepted) {
+            n_ls_fail++;
+            if (++consecutive_fail >= 5) { status = 2; break; }
+        } else consecutive_fail = 0;
+        n_soc += soc_used;
+        /* ---- update ---- */
+        for (size_t i = 0; i < NX1; i++) S->x[i] += alpha * S->dx[i];
+        for (size_t i = 0; i < NU; i++) S->u[i] += alpha * S->du[i];
+        for (size_t i = 0; i < NI; i++) { S->s[i] += alpha * S->ds[i]; S->yi[i] += alpha * S->dyi[i]; }
+        for (int i = 0; i < N * nx; i++) S->lam[i] += alpha * S->dlam[i];
+        for (size_t i = 0; i < NE; i++) S->ye[i] += alpha * S->dye[i];
+#define ZUPD(z, dz, slack)                                                                    \
+    do {                                                                                      \
+        double zz = (z) + az * (dz), sl = (slack);                                            \
+        (z) = fmax(fmin(zz, kappa_sigma * mu / sl), mu / (kappa_sigma * sl));                  \
+    } while (0)
+        for (int k = 1; k <= N; k++)
+            for (int j = 0; j < nx; j++) {
+                const int i = k * nx + j;
+                if (hasb(S->xlo[j])) ZUPD(S->zxL[i], S->dzxL[i], S->x[i] - S->xlo[j]);
+                if (hasb(S->xhi[j])) ZUPD(S->zxU[i], S->dzxU[i], S->xhi[j] - S->x[i]);
+            }
+        for (int i = 0; i < N * nu; i++) {
+            if (S->ufix[i]) continue;
+            if (hasb(S->ulo[i])) ZUPD(S->zuL[i], S->dzuL[i], S->u[i] - S->ulo[i]);
+            if (hasb(S->uhi[i])) ZUPD(S->zuU[i], S->dzuU[i], S->uhi[i] - S->u[i]);
+        }
+        for (int i = 0; i < N * ni; i++) {
+            if (hasb(S->clo[i])) ZUPD(S->vL[i], S->dvL[i], S->s[i] - S->clo[i]);
+            if (hasb(S->chi[i])) ZUPD(S->vU[i], S->dvU[i], S->chi[i] - S->s[i]);
+        }
+#undef ZUPD
+    }
+    /* ---- output in the reference layout [x_0 | (u_k, x_{k+1}) x N] ---- */
+    if (w_out) {
+        double *o = w_out;
+        memcpy(o, S->x, nx * sizeof(double));
+        o += nx;
+        for (int k = 0; k < N; k++) {
+            memcpy(o, S->u + k * nu, nu * sizeof(double));
+            o += nu;
+            memcpy(o, S->x + (k + 1) * nx, nx * sizeof(double));
+            o += nx;
+        }
+    }
+    if (res) {
+        double fo = 0;
+        for (int k = 0; k < N; k++) {
+            double l, ci[GI], ce[GE], f[GX];
+            eval_values(S, k, S->x + k * nx, S->u + k * nu, &l, ci, ce, f);
+            fo += l;
+        }
+        res->status = status; res->iter = it; res->kkt = E0; res->cviol = cviol; res->obj = fo; res->mu = mu;
+        res->n_ls_fail = n_ls_fail; res->n_inertia_fix = n_ic;
+    }
+    if (O->verbose) fprintf(stderr, "second-order corrections accepted: %d\n", n_soc);
+    double **pp[] = {&S->ulo, &S->uhi, &S->clo, &S->chi, &S->x, &S->u, &S->s, &S->lam, &S->ye, &S->yi, &S->zxL,
+                     &S->zxU, &S->zuL, &S->zuU, &S->vL, &S->vU, &S->tx, &S->tu, &S->ts, &S->l, &S->gl, &S->ci,
+                     &S->Ji, &S->ce, &S->Je, &S->f, &S->Af, &S->Bf, &S->W, &S->dx, &S->du, &S->ds, &S->dlam,
+                     &S->dye, &S->dyi, &S->dzxL, &S->dzxU, &S->dzuL, &S->dzuU, &S->dvL, &S->dvU, &S->Sx, &S->gx,
+                     &S->Su, &S->gu, &S->Ss, &S->gs, &S->wv, &S->G, &S->Dsave, &S->rdyn, &S->rin, &S->req,
+                     &S->trdyn, &S->trin, &S->treq, &S->sdyn, &S->sin_, &S->seq, &S->bk};
+    for (size_t i = 0; i < sizeof pp / sizeof pp[0]; i++) free(*pp[i]);
+    free(S->ufix); free(S->perm); free(S->piv);
+    return 0;
+}
+
+/* Node values and derivatives for tests: l, c_in, c_eq, f and their Jacobians w.r.t. [x|u]
+ * (row-major), and the Hessian of l + yi.c_in + ye.c_eq + lam.f (nv x nv). */
+int mfg_node_derivs(const double *blob0, const double *blob1, const mfg_ocp *P, const double *xu, const double *yi,
+                    const double *ye, const double *lam, double *vals, double *jac, double *H) {
+    models_t MM;
+    memset(&MM, 0, sizeof MM);
+    if (mfo_model_from_blob(blob0, &MM.M[0])) return -1;
+    frame_from_arr(P->frame[0], &MM.F[0]);
+    if (P->family == MFG_BOX) {
+        if (!blob1 || mfo_model_from_blob(blob1, &MM.M[1])) return -1;
+        frame_from_arr(P->frame[1], &MM.F[1]);
+    }
+    const int nx = P->nx, nv = P->nx + P->nu, ni = P->ni, ne = P->ne, no = 1 + ni + ne + nx;
+    for (int a = 0; a < nv; a++)
+        for (int b = a; b < nv; b++) {
+            hd hx[GV], hl, hci[GI], hce[GE], hf[GX];
+            for (int i = 0; i < nv; i++) hx[i] = K(xu[i]);
+            hx[a].b = 1.0;
+            hx[b].c = 1.0;
+            node_hd(P, &MM, hx, &hl, hci, hce, hf);
+            double h2 = hl.d;
+            for (int r = 0; r < ni; r++) h2 += yi[r] * hci[r].d;
+            for (int e = 0; e < ne; e++) h2 += ye[e] * hce[e].d;
+            for (int j = 0; j < nx; j++) h2 += lam[j] * hf[j].d;
+            H[a * nv + b] = H[b * nv + a] = h2;
+            if (a == b) {
+                jac[0 * nv + a] = hl.b;
+                for (int r = 0; r < ni; r++) jac[(1 + r) * nv + a] = hci[r].b;
+                for (int e = 0; e < ne; e++) jac[(1 + ni + e) * nv + a] = hce[e].b;
+                for (int j = 0; j < nx; j++) jac[(1 + ni + ne + j) * nv + a] = hf[j].b;
+                if (a == 0) {
+                    vals[0] = hl.a;
+                    for (int r = 0; r < ni; r++) vals[1 + r] = hci[r].a;
+                    for (int e = 0; e < ne; e++) vals[1 + ni + e] = hce[e].a;
+                    for (int j = 0; j < nx; j++) vals[1 + ni + ne + j] = hf[j].a;
+                }
+            }
+        }
+    (void)no;
+    return 0;
+}
+
+/* Batch of independent horizons (OpenMP over problems when nthreads > 0, nodes otherwise). */
+int mfg_solve_batch(const double *blob0, const double *blob1, const mfg_ocp *P, int batch, const mfg_opts *O,
+                    double *w_out, int w_stride, mfg_result *res, int nthreads) {
+    int err = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(| : err)
+#endif
+    for (int b = 0; b < batch; b++)
+        err |= mfg_solve(blob0, blob1, &P[b], O, w_out ? w_out + (size_t)b * w_stride : NULL, &res[b]);
+    return err;
+}

@@ -23,7 +23,8 @@ BLOB_JSTRIDE = 33
 
 
 def build(force: bool = False) -> str:
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(HERE, "mf_oracle.c")):
+    srcs = [os.path.join(HERE, f) for f in ("mf_oracle.c", "mf_ocp.c", "hd_kin.h", "Makefile")]
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
     return LIB
 
