@@ -1,0 +1,146 @@
+"""Node records of the generic families (csrc/gfam.hpp) vs the oracle, on the CPU.
+
+tests/native/famcheck.cpp instantiates, for the host, exactly the functions the device kernel
+k_geval runs (pre-pass, seeds, one forward-over-reverse lane per tangent direction, record
+entries), so the record -- values, cost gradient, constraint Jacobians, dynamics Jacobians and the
+exact Lagrangian Hessian assembled from lane columns plus closed-form algebraic terms -- can be
+compared with the oracle's hyper-dual restatement (oracle/mf_ocp.c mfg_node_derivs) without a GPU.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from mpc_fatigue_amd import problems as PR
+from oracle import generic as G
+from tests.conftest import ROOT
+
+NATIVE = os.path.join(ROOT, "tests", "native")
+LIB = os.path.join(NATIVE, "libfamcheck.so")
+CSRC = os.path.join(ROOT, "mpc_fatigue_amd", "csrc")
+GX = 32
+
+
+class GParams(C.Structure):
+    """Mirror of mf::GParams (csrc/gfam.hpp)."""
+    _fields_ = [("N", C.c_int), ("h", C.c_double), ("eq_from", C.c_int),
+                ("nf", C.c_int), ("use_line", C.c_int), ("thermal", C.c_int), ("fdir", C.c_double * 9),
+                ("wF", C.c_double), ("wqd", C.c_double), ("wtau", C.c_double), ("wT", C.c_double),
+                ("th_a", C.c_double), ("th_b", C.c_double), ("Ra", C.c_double), ("Rh", C.c_double),
+                ("ktau", C.c_double * 16),
+                ("box_mg", C.c_double), ("box_L", C.c_double), ("box_pdes", C.c_double * 3), ("w_box", C.c_double),
+                ("w_qdb", C.c_double),
+                ("x_lo", C.c_double * GX), ("x_hi", C.c_double * GX),
+                ("tol", C.c_double), ("constr_viol_tol", C.c_double), ("mu_init", C.c_double), ("F_init", C.c_double),
+                ("max_iter", C.c_int), ("max_soc", C.c_int), ("init_zero", C.c_int), ("has_u_init", C.c_int),
+                ("u_init", C.c_double * GX)]
+
+
+def _build():
+    src = [os.path.join(NATIVE, "famcheck.cpp"), os.path.join(CSRC, "urdf.cpp")]
+    deps = src + [os.path.join(CSRC, h) for h in ("gfam.hpp", "adj.hpp", "dyn.hpp", "model.hpp")]
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):
+        return
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    subprocess.check_call([hipcc, "-O2", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950",
+                           "-x", "hip", src[0], "-x", "hip", src[1], "-o", LIB])
+
+
+@pytest.fixture(scope="module")
+def fam():
+    _build()
+    L = C.CDLL(LIB)
+    L.fam_node_record.restype = C.c_int
+    assert L.fam_gparams_size() == C.sizeof(GParams)
+    return L
+
+
+def _p(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def gparams(spec):
+    g = GParams()
+    g.N, g.h, g.eq_from = spec["N"], spec["h"], 2
+    if spec.get("family") == "box":
+        g.box_mg, g.box_L, g.w_box, g.w_qdb = spec["box_mg"], spec["box_L"], spec["w_box"], spec["w_qd"]
+        g.box_pdes[:] = list(spec["p_des"])
+    else:
+        g.nf, g.use_line, g.thermal = spec["nf"], int(spec["use_line"]), int(spec.get("thermal", False))
+        fd = np.zeros(9)
+        fd[:3 * spec["nf"]] = np.asarray(spec["fdir"], float).reshape(-1)
+        g.fdir[:] = list(fd)
+        g.wF, g.wqd, g.wtau = spec["wF"], spec["wqd"], spec["wtau"]
+        if g.thermal:
+            g.th_a, g.th_b, g.Ra, g.Rh = spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+            kt = np.zeros(16)
+            kt[:6] = spec["ktau"]
+            g.ktau[:] = list(kt)
+    return g
+
+
+def compare(fam, family, spec, xu, nx, nu, ni, ne, seed=0):
+    rng = np.random.default_rng(seed)
+    yi, ye, lam = rng.normal(size=ni) * 10, rng.normal(size=max(ne, 1)), rng.normal(size=nx)
+    urdfs = spec["urdf"] if isinstance(spec["urdf"], list) else [spec["urdf"], spec["urdf"]]
+    x0 = open(PR.urdf_path(urdfs[0])).read().encode()
+    x1 = open(PR.urdf_path(urdfs[1])).read().encode()
+    nv = nx + nu
+    rec = np.zeros(4096)
+    lref = np.asarray(spec.get("line_ref", [0.0, 0.0]), float)
+    g = gparams(spec)
+    n = fam.fam_node_record(family, x0, x1, spec["frame"].encode(), C.byref(g), _p(np.ascontiguousarray(xu)),
+                            _p(yi), _p(ye), _p(lam), _p(lref), _p(rec))
+    assert n > 0
+    vals, jac, H = G.node_derivs(spec, xu, yi, ye, lam)
+    o = 0
+    l = rec[o]; o += 1
+    gl = rec[o:o + nv]; o += nv
+    ci = rec[o:o + ni]; o += ni
+    Ji = rec[o:o + ni * nv].reshape(ni, nv); o += ni * nv
+    ce = rec[o:o + ne]; o += ne
+    Je = rec[o:o + ne * nx].reshape(ne, nx); o += ne * nx
+    f = rec[o:o + nx]; o += nx
+    A = rec[o:o + nx * nx].reshape(nx, nx); o += nx * nx
+    B = rec[o:o + nx * nu].reshape(nx, nu); o += nx * nu
+    W = rec[o:o + nv * nv].reshape(nv, nv); o += nv * nv
+    assert o == n
+    sc = lambda a: max(1.0, np.abs(a).max())
+    np.testing.assert_allclose(l, vals[0], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(ci, vals[1:1 + ni], atol=1e-11 * sc(ci))
+    np.testing.assert_allclose(ce, vals[1 + ni:1 + ni + ne], atol=1e-12)
+    np.testing.assert_allclose(f, vals[1 + ni + ne:], atol=1e-12 * sc(f))
+    np.testing.assert_allclose(gl, jac[0], atol=1e-11 * sc(jac[0]))
+    np.testing.assert_allclose(Ji, jac[1:1 + ni], atol=1e-11 * sc(Ji))
+    np.testing.assert_allclose(Je, jac[1 + ni:1 + ni + ne, :nx], atol=1e-12 * sc(Je))
+    np.testing.assert_allclose(A, jac[1 + ni + ne:, :nx], atol=1e-12 * sc(A))
+    np.testing.assert_allclose(B, jac[1 + ni + ne:, nx:], atol=1e-12 * sc(B))
+    np.testing.assert_allclose(W, H, atol=1e-10 * sc(H))
+    np.testing.assert_allclose(W, W.T, atol=1e-11 * sc(W))
+
+
+@pytest.mark.parametrize("k", [0, 17, 40])
+def test_box_record_matches_oracle(fam, golden, k):
+    g, _ = golden["G1_box_N50"]
+    xu = g[k * 30:k * 30 + 30].copy()
+    if k == 0:
+        xu[12:24] = np.random.default_rng(2).uniform(-1, 0.5, 12)  # non-zero velocities
+    compare(fam, 0, PR.box_dual(N=1), xu, 12, 18, 18, 1, seed=k)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_chain_record_matches_oracle(fam, seed):
+    rng = np.random.default_rng(seed)
+    spec = dict(PR.pilz6_bench(N=1), wtau=0.3, wqd=2.0)
+    xu = np.r_[rng.normal(size=6), 0.3 * rng.normal(size=6), [20.0]]
+    compare(fam, 1, spec, xu, 6, 7, 6, 2, seed=seed)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_thermal_record_matches_oracle(fam, seed):
+    rng = np.random.default_rng(10 + seed)
+    spec = dict(PR.pilz6_thermal(N=1), wtau=0.1)
+    xu = np.r_[rng.normal(size=6), 60 + rng.normal(size=6), 0.3 * rng.normal(size=6), [40.0]]
+    compare(fam, 2, spec, xu, 12, 7, 6, 2, seed=seed)
