@@ -161,6 +161,79 @@ int mf_problem_timing(mf_problem *p, int enable);
 int mf_problem_kernel_stats(const mf_problem *p, double *ms_total, long *launches);
 const char *mf_kernel_name(int slot);
 
+/* ---- generic stage-structured OCPs: dual-arm box (C3), thermal fatigue state (a8) ----
+ * Replaces the per-node transcription loops of python/2_pilz_6_DOF/Box_Pilz_6DOF.py:219-456 and of
+ * the thermal MPC (python/Centauro_script/RepeatedMPCwithThermal.py:183-402, Tmodel_library.py:9-41)
+ * plus their nlpsol('ipopt') solves.  One horizon is the NLP
+ *   w = [x_0 | (u_k, x_{k+1}) for k < N]   (the reference's CSV layout, Box_Pilz_6DOF.py:464-466)
+ *   min sum_k l(x_k, u_k)   s.t.  x_{k+1} = f(x_k, u_k),  c_lo[k] <= c_in(x_k, u_k) <= c_hi[k],
+ *   c_eq(x_k) = 0 (eq_from <= k < N),  x_lo <= x_k <= x_hi (k >= 1),  u_lo[k] <= u_k <= u_hi[k]
+ * where u_lo == u_hi fixes a component (qd_0).  Families:
+ *   MF_FAM_CHAIN  x = [q, (T)], u = [qd, F];  c_in = tau = ID(q, qd, 0) - J_f^T [sum F_a fdir_a; 0];
+ *                 c_eq = p_f[0:2] - line_ref;  l = wF|F|^2 + wqd|qd|^2 + wtau|tau|^2 + wT|T|^2;
+ *                 f = [q + h qd, th_a T + th_b (Ra (tau/ktau)^2 + qd^2/Rh)]   (thermal: nx = 2n)
+ *   MF_FAM_BOX    two 6-DOF arms (model 0 = first, model 1 = second URDF), x = [q_L, q_R],
+ *                 u = [qd_L, qd_R, F_L, F_R];  c_in = [F_L + F_R - (0, 0, m g) as (z, x, y),
+ *                 (E1 - E2) x (F_L - F_R), tau_L, tau_R];  c_eq = |E1 - E2|^2 - L;
+ *                 l = w_box |(E1 + E2)/2 - p_des|^2 + w_qd |qd|^2;  f = q + h qd            */
+#define MF_FAM_CHAIN 0
+#define MF_FAM_BOX 1
+#define MF_GX_MAX 32
+typedef struct mf_gproblem mf_gproblem;
+typedef struct {
+    int family;            /* MF_FAM_* */
+    int N;
+    double h;
+    int frame0, frame1;    /* mf_frame_id of the force / constraint frame in model 0 / model 1 */
+    int eq_from;           /* first node carrying c_eq (2: q_0 and q_1 = q_0 + h qd_0 are fixed data) */
+    int nf;                /* CHAIN: force components along fdir */
+    double fdir[9];
+    int use_line;
+    double line_ref[2];    /* default line reference (per-problem override in mf_gsolve_batch) */
+    double wF, wqd, wtau, wT;
+    int thermal;
+    double th_a, th_b, Ra, Rh;
+    double ktau[MF_MAX_JOINTS];
+    double box_mg, box_L, box_pdes[3], w_box, w_qd;  /* BOX */
+    double x_lo[MF_GX_MAX], x_hi[MF_GX_MAX];         /* states k >= 1, +-inf allowed */
+    const double *u_lo, *u_hi;                       /* N x nu */
+    const double *c_lo, *c_hi;                       /* N x ni */
+} mf_gspec;
+
+typedef struct {
+    double tol;            /* scaled KKT error (IPOPT E_0) */
+    double constr_viol_tol;
+    int max_iter;
+    double mu_init;
+    int init_zero;         /* 1: IPOPT's x0 = 0 for every free variable; 0: hold x_0 */
+    double F_init;         /* initial force components when u_init is NULL */
+    const double *u_init;  /* nu initial controls used at every node (host memory), or NULL */
+    int max_soc;           /* second-order corrections per iteration (IPOPT max_soc; 0 = off) */
+    int verbose;
+} mf_gopts;
+
+int mf_gproblem_create(const mf_model *m0, const mf_model *m1, const mf_gspec *spec, mf_gproblem **out);
+void mf_gproblem_free(mf_gproblem *p);
+/* dims = {nx, nu, ni, ne, wsize} */
+int mf_gproblem_dims(const mf_gproblem *p, int *dims5);
+/* x0: batch x nx; u0: batch x nu values of the fixed controls at k = 0 (qd_0 carried by a receding
+ * horizon, mpc_principal.py:365-374) or NULL = u_lo[0]; w0: batch x wsize warm start (primal) or NULL;
+ * line_ref: batch x 2 or NULL.  Outputs as mf_solve_batch.  Host memory; _dev: device memory on stream. */
+int mf_gsolve_batch(mf_gproblem *p, int batch, const double *x0, const double *u0, const double *w0,
+                    const double *line_ref, const mf_gopts *opts, double *w, int *status, int *iters, double *kkt,
+                    double *obj, int device);
+int mf_gsolve_batch_dev(mf_gproblem *p, int batch, const double *x0, const double *u0, const double *w0,
+                        const double *line_ref, const mf_gopts *opts, double *w, int *status, int *iters,
+                        double *kkt, double *obj, void *stream);
+/* One node record evaluated by the device kernel (tests): xu = [x | u], multipliers yi (ni), ye (ne),
+ * lam (nx); rec = [l | grad l (nv) | c_in (ni) | d c_in (ni x nv) | c_eq (ne) | d c_eq / dx (ne x nx) |
+ * f (nx) | A (nx x nx) | B (nx x nu) | W (nv x nv)], row-major blocks.  Returns the record size. */
+int mf_gnode_record(mf_gproblem *p, const double *xu, const double *yi, const double *ye, const double *lam,
+                    const double *line_ref, double *rec, int device);
+/* Diagnostics: dual state of problem b after the last solve, [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU |
+ * mu] (per-node blocks as the solver stores them).  Returns the number of doubles written. */
+int mf_gdebug_duals(mf_gproblem *p, int b, double *out);
+
 const char *mf_last_error(void);
 
 #ifdef __cplusplus

@@ -49,6 +49,32 @@ class ProblemSpec(C.Structure):
     ]
 
 
+MF_GX_MAX = 32
+
+
+class GSpec(C.Structure):
+    """mf_gspec (include/mpcfatigue.h): generic stage-structured OCP (box C3, thermal a8)."""
+    _fields_ = [
+        ("family", C.c_int), ("N", C.c_int), ("h", C.c_double), ("frame0", C.c_int), ("frame1", C.c_int),
+        ("eq_from", C.c_int), ("nf", C.c_int), ("fdir", C.c_double * 9), ("use_line", C.c_int),
+        ("line_ref", C.c_double * 2), ("wF", C.c_double), ("wqd", C.c_double), ("wtau", C.c_double),
+        ("wT", C.c_double), ("thermal", C.c_int), ("th_a", C.c_double), ("th_b", C.c_double), ("Ra", C.c_double),
+        ("Rh", C.c_double), ("ktau", C.c_double * MF_MAX_JOINTS),
+        ("box_mg", C.c_double), ("box_L", C.c_double), ("box_pdes", C.c_double * 3), ("w_box", C.c_double),
+        ("w_qd", C.c_double),
+        ("x_lo", C.c_double * MF_GX_MAX), ("x_hi", C.c_double * MF_GX_MAX),
+        ("u_lo", C.POINTER(C.c_double)), ("u_hi", C.POINTER(C.c_double)),
+        ("c_lo", C.POINTER(C.c_double)), ("c_hi", C.POINTER(C.c_double)),
+    ]
+
+
+class GOpts(C.Structure):
+    """mf_gopts (include/mpcfatigue.h)."""
+    _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
+                ("mu_init", C.c_double), ("init_zero", C.c_int), ("F_init", C.c_double),
+                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("verbose", C.c_int)]
+
+
 class SolverOpts(C.Structure):
     _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
                 ("mu_init", C.c_double), ("F_init", C.c_double), ("verbose", C.c_int)]
@@ -92,6 +118,13 @@ def lib() -> C.CDLL:
         "mf_ik_batch": ([vp, C.c_int, dp, dp, dp, dp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double], C.c_int),
         "mf_ik_batch_dev": ([vp, C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, vp],
                             C.c_int),
+        "mf_gproblem_create": ([vp, vp, C.POINTER(GSpec), C.POINTER(vp)], C.c_int),
+        "mf_gproblem_free": ([vp], None),
+        "mf_gproblem_dims": ([vp, ip], C.c_int),
+        "mf_gsolve_batch": ([vp, C.c_int, dp, dp, dp, dp, C.POINTER(GOpts), dp, ip, ip, dp, dp, C.c_int], C.c_int),
+        "mf_gsolve_batch_dev": ([vp, C.c_int, vp, vp, vp, vp, C.POINTER(GOpts), vp, vp, vp, vp, vp, vp], C.c_int),
+        "mf_gnode_record": ([vp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
+        "mf_gdebug_duals": ([vp, C.c_int, dp], C.c_int),
         "mf_last_error": ([], cp),
     }
     for name, (argt, rest) in sig.items():
@@ -108,6 +141,8 @@ EXPORTED_SYMBOLS = [
     "mf_problem_wsize", "mf_node_eval", "mf_solve_batch", "mf_solve_batch_dev", "mf_solve_batch_ws",
     "mf_solve_batch_ws_dev", "mf_problem_timing",
     "mf_problem_kernel_stats", "mf_kernel_name", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
+    "mf_gproblem_create", "mf_gproblem_free", "mf_gproblem_dims", "mf_gsolve_batch", "mf_gsolve_batch_dev",
+    "mf_gnode_record", "mf_gdebug_duals",
 ]
 
 

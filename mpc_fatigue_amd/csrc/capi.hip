@@ -75,6 +75,20 @@ static int frame_dev(mf_model *m, int frame, DevFrame **out) {
     return MF_OK;
 }
 
+// ---- internal entry points for the generic solver (csrc/capi_internal.hpp)
+namespace mf {
+int capi_fail(int code, const std::string &msg) { return fail(code, msg); }
+int capi_model_dev(mf_model *m, const DevModel **dev, const Model **host) {
+    int e = upload_model(m);
+    if (e) return e;
+    if (dev) *dev = m->d_model;
+    if (host) *host = &m->host;
+    return MF_OK;
+}
+int capi_frame_dev(mf_model *m, int frame, DevFrame **out) { return frame_dev(m, frame, out); }
+int capi_ensure_device() { return ensure_device(); }
+}  // namespace mf
+
 extern "C" int mf_model_from_urdf(const char *urdf_xml, mf_model **out) {
     if (!urdf_xml || !out) return fail(MF_ERR_ARG, "null argument");
     try {

@@ -48,6 +48,7 @@ struct GParams {
     double tol, constr_viol_tol, mu_init, F_init;
     int max_iter, max_soc, init_zero, has_u_init;
     double u_init[GX_MAX];
+    int force_from, tier1_from, tier1_to;  // first force control; u range regularised first (concave cost)
 };
 
 template <int NX_, int NU_, int NI_, int NE_> struct GDims {
@@ -131,7 +132,7 @@ MF_HD double skew_el(const double *y, int r, int c) {  // [y]x (r, c)
 
 // ================================================================ BoxFam (C3)
 struct BoxFam {
-    static constexpr int NJ = 6, NARM = 2, NDIR = 2 * NJ;
+    static constexpr int NJ = 6, NARM = 2, NDIR = 2 * NJ, NM = 2;
     using D = GDims<12, 18, 18, 1>;
     static constexpr int LANES = NARM * NDIR;  // derivative lanes per node
     static constexpr int LCOL = GLaneOut<NJ>::LCOL;
@@ -149,7 +150,7 @@ struct BoxFam {
     }
 
     // values at (x, u): l, ci, ce, f (line search / slacks).  E: frame points out (may be null)
-    MF_HD static void values(const DevModel *M, const DevFrame *F, const GParams &P, const double *x, const double *u,
+    template <class MA, class FA> MF_HD static void values(MA M, FA F, const GParams &P, const double *x, const double *u,
                              const double *, double &l, double *ci, double *ce, double *f) {
         double tL[NJ], tR[NJ], E1[3], E2[3];
         arm_values<NJ>(M[0], F[0], x, u, u + 12, tL, E1);
@@ -178,7 +179,7 @@ struct BoxFam {
 
     static constexpr int PRE = NARM;  // pre-pass lanes per node
     // pre-pass lane a: frame point E_a and tau_a at the node
-    MF_HD static void prepass(const DevModel *M, const DevFrame *F, const GParams &, const double *x, const double *u,
+    template <class MA, class FA> MF_HD static void prepass(MA M, FA F, const GParams &, const double *x, const double *u,
                               int a, Scratch &S) {
         arm_values<NJ>(M[a], F[a], x + 6 * a, u + 6 * a, u + 12 + 3 * a, S.tau[a], S.E[a]);
     }
@@ -201,7 +202,7 @@ struct BoxFam {
         }
     }
     // derivative lane t in [0, LANES): arm t / NDIR, direction t % NDIR
-    MF_HD static void lane(const DevModel *M, const DevFrame *F, const double *x, const double *u, const double *yi,
+    template <class MA, class FA> MF_HD static void lane(MA M, FA F, const double *x, const double *u, const double *yi,
                            int t, Scratch &S) {
         const int a = t / NDIR, v = t % NDIR;
         arm_lane<NJ>(M[a], F[a], x + 6 * a, u + 6 * a, u + 12 + 3 * a, yi + 6 + 6 * a, S.seed[a], v, S.col[a][v]);
@@ -335,7 +336,7 @@ struct BoxFam {
 
 // ================================================================ ChainFam (C1, C2, thermal)
 template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
-    static constexpr int NJ = NJ_, NF = NF_, NDIR = 2 * NJ_;
+    static constexpr int NJ = NJ_, NF = NF_, NDIR = 2 * NJ_, NM = 1;
     static constexpr bool TH = THERMAL_;
     using D = GDims<(THERMAL_ ? 2 : 1) * NJ_, NJ_ + NF_, NJ_, NE_>;
     static constexpr int LANES = NDIR;
@@ -363,7 +364,7 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
         const double ia = tau / P.ktau[j];
         return P.Ra * ia * ia + qd * qd / P.Rh;
     }
-    MF_HD static void values(const DevModel *M, const DevFrame *F, const GParams &P, const double *x, const double *u,
+    template <class MA, class FA> MF_HD static void values(MA M, FA F, const GParams &P, const double *x, const double *u,
                              const double *lref, double &l, double *ci, double *ce, double *f) {
         double tau[NJ], pf[3], Fw[3];
         world_force(P, u, Fw);
@@ -383,7 +384,7 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
         l = c;
     }
     static constexpr int PRE = 1;
-    MF_HD static void prepass(const DevModel *M, const DevFrame *F, const GParams &P, const double *x, const double *u,
+    template <class MA, class FA> MF_HD static void prepass(MA M, FA F, const GParams &P, const double *x, const double *u,
                               int, Scratch &S) {
         world_force(P, u, S.Fw);
         arm_values<NJ>(M[0], F[0], x, u, S.Fw, S.tau[0], S.pf);
@@ -400,7 +401,7 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
         }
         for (int r = 0; r < 3; r++) S.seed[r] = (eqon && r < NE_) ? ye[r] : 0.0;
     }
-    MF_HD static void lane(const DevModel *M, const DevFrame *F, const double *x, const double *u, const double *, int v,
+    template <class MA, class FA> MF_HD static void lane(MA M, FA F, const double *x, const double *u, const double *, int v,
                            Scratch &S) {
         arm_lane<NJ>(M[0], F[0], x, u, S.Fw, S.cw, S.seed, v, S.col[0][v]);
     }

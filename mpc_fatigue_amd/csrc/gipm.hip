@@ -1,0 +1,1409 @@
+// Generic batched interior-point solver for stage-structured OCPs on MI355X (gfx950):
+// the dual-arm box (C3, python/2_pilz_6_DOF/Box_Pilz_6DOF.py:219-456) and the thermal-fatigue
+// transcriptions (Tmodel_library.py:9-41, RepeatedMPCwithThermal.py:371-376), plus the Pilz chain
+// tasks through the same path.  The iteration is the one of DESIGN.md section 4 (IPOPT-style
+// primal-dual interior point, monotone mu, inertia correction, l1-merit line search with IPOPT's
+// second-order corrections); the CPU restatement is oracle/mf_ocp.c (block-tridiagonal
+// Bunch-Kaufman), this file factorises the same KKT matrix by a Riccati recursion with general
+// dynamics Jacobians A_k, B_k.
+//
+// One iteration = two launches:
+//   k_geval<FAM>  lanes (problem, node, tangent direction): the node record (gfam.hpp) --
+//                 forward-over-reverse sweeps per arm and direction, assembled in LDS, written as
+//                 one contiguous record per node
+//   k_giter<FAM>  one wavefront per horizon: optimality error, barrier update, inertia-corrected
+//                 Riccati factorisation (stage blocks [[Quu, Du^T], [Du, -dc]] by Bunch-Kaufman in
+//                 LDS), solve, fraction to the boundary, line search (trial values: one lane per
+//                 node) with second-order corrections, update
+// Layout: every per-problem array is [problem][node][field]; a node's record is contiguous.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "bk_wave.hpp"
+#include "capi_internal.hpp"
+#include "gfam.hpp"
+
+namespace mf {
+
+struct GState {
+    double mu, nu, reg_last, E0, cviol, obj;
+    int reg_tier, status, iter, n_ls_fail, n_ic, consec_fail, n_soc, pad;
+};
+enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INERTIA = 3 };
+
+struct GArrays {
+    double *x, *u, *s, *lam, *ye, *yi, *zxL, *zxU, *zuL, *zuU, *vL, *vU;
+    double *dx, *du, *ds, *dlam, *dye, *dyi, *dzxL, *dzxU, *dzuL, *dzuU, *dvL, *dvU;
+    double *bk;     // saved direction (second-order corrections)
+    double *rec;    // node records
+    double *Sx, *gx, *Su, *gu, *Ss, *gs;
+    double *rdyn, *rin, *req, *trdyn, *trin, *treq, *sdyn, *sin_, *seq;
+    double *tx, *tu, *ts;
+    double *P, *Kinv, *Kfb, *pv, *kv;
+    const double *u_lo, *u_hi, *c_lo, *c_hi;  // shared, N x NU / N x NI
+    double *x0, *lref;                        // per problem: NX, 2
+    const double *u0, *w0;                    // optional per-problem fixed u_0 values / warm start
+    GState *st;
+    int *active;
+};
+
+template <class D> struct GSz {
+    static constexpr int NX = D::NX, NU = D::NU, NI = D::NIA, NE = D::NEA, NK = D::NU + D::NEA;
+    size_t N;
+    __host__ __device__ GSz(int n) : N(n) {}
+    __host__ __device__ size_t x() const { return (N + 1) * NX; }
+    __host__ __device__ size_t u() const { return N * NU; }
+    __host__ __device__ size_t i() const { return N * NI; }
+    __host__ __device__ size_t e() const { return N * NE; }
+    __host__ __device__ size_t l() const { return N * NX; }
+    __host__ __device__ size_t rec() const { return N * D::REC; }
+    __host__ __device__ size_t bk() const { return 3 * x() + 3 * u() + 4 * i() + l() + e(); }
+    __host__ __device__ size_t P() const { return N * NX * NX; }
+    __host__ __device__ size_t Kinv() const { return N * (NK * (NK + 1) + 2 * NK); }  // BK factor + perm/piv
+    __host__ __device__ size_t Kfb() const { return N * NK * NX; }
+    __host__ __device__ size_t kv() const { return N * NK; }
+};
+
+__device__ __forceinline__ bool gb(double b) { return isfinite(b); }
+
+__device__ __forceinline__ double gpush(double x, double lo, double hi) {
+    const double k1 = 1e-2, k2 = 1e-2;
+    const bool hl = gb(lo), hh = gb(hi);
+    if (hl && hh) {
+        const double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
+        const double pu = fmin(k1 * fmax(1.0, fabs(hi)), k2 * (hi - lo));
+        x = fmax(x, lo + pl);
+        x = fmin(x, hi - pu);
+    } else if (hl) {
+        x = fmax(x, lo + k1 * fmax(1.0, fabs(lo)));
+    } else if (hh) {
+        x = fmin(x, hi - k1 * fmax(1.0, fabs(hi)));
+    }
+    return x;
+}
+
+__device__ __forceinline__ void gsync() {
+    __threadfence_block();
+    __syncthreads();
+}
+
+// first NJ joints of a DevModel in LDS
+template <int NJ> struct GModelLds {
+    static constexpr int WORDS = (int)((offsetof(DevModel, j) + NJ * sizeof(DevJoint) + sizeof(double) - 1) / sizeof(double));
+    double w[WORDS];
+    __device__ void load(const DevModel *g) {
+        const double *s = reinterpret_cast<const double *>(g);
+        for (int i = threadIdx.x; i < WORDS; i += blockDim.x) w[i] = s[i];
+    }
+    __device__ const DevModel &get() const { return *reinterpret_cast<const DevModel *>(w); }
+};
+
+template <class FAM> struct GModels {
+    GModelLds<FAM::NJ> m[FAM::NM];
+    DevFrame f[FAM::NM];
+    __device__ void load(const DevModel *M0, const DevModel *M1, const DevFrame *F0, const DevFrame *F1) {
+        m[0].load(M0);
+        if (FAM::NM > 1) m[FAM::NM - 1].load(M1);
+        const double *s0 = reinterpret_cast<const double *>(F0);
+        double *d0 = reinterpret_cast<double *>(&f[0]);
+        for (int i = threadIdx.x; i < (int)(sizeof(DevFrame) / sizeof(double)); i += blockDim.x) d0[i] = s0[i];
+        if (FAM::NM > 1) {
+            const double *s1 = reinterpret_cast<const double *>(F1);
+            double *d1 = reinterpret_cast<double *>(&f[FAM::NM - 1]);
+            for (int i = threadIdx.x; i < (int)(sizeof(DevFrame) / sizeof(double)); i += blockDim.x) d1[i] = s1[i];
+        }
+    }
+};
+
+// the family functions take DevModel / DevFrame arrays indexed by arm; in LDS the images are
+// separate objects, so a small adaptor forwards by arm
+// (two named members and a select, not a pointer array: a lane-indexed array of pointers is a
+// private alloca that the backend promotes into a per-thread LDS table)
+struct MArr {
+    const DevModel *p0, *p1;
+    __device__ __forceinline__ const DevModel &operator[](int a) const { return a ? *p1 : *p0; }
+};
+struct FArr {
+    const DevFrame *p0, *p1;
+    __device__ __forceinline__ const DevFrame &operator[](int a) const { return a ? *p1 : *p0; }
+};
+
+
+#define GMODELS(FAM)                                                                               \
+    __shared__ GModels<FAM> Gm;                                                                    \
+    Gm.load(M0, M1, F0, F1);                                                                       \
+    __syncthreads();                                                                               \
+    const MArr M{&Gm.m[0].get(), &Gm.m[FAM::NM - 1].get()};                                        \
+    const FArr F{&Gm.f[0], &Gm.f[FAM::NM - 1]}
+
+// ============================================================== node records
+template <class FAM>
+__global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                               const DevFrame *F1, GParams P, GArrays A, int batch) {
+    using D = typename FAM::D;
+    constexpr int L = FAM::LANES, NPB = 256 / L;
+    GMODELS(FAM);
+    __shared__ typename FAM::Scratch S[NPB];
+    const int tid = threadIdx.x, g = tid / L, t = tid % L;
+    const int N = P.N;
+    const long node = (long)blockIdx.x * NPB + g;
+    bool run = g < NPB && node < (long)batch * N;
+    int b = 0, k = 0;
+    if (run) {
+        b = (int)(node / N);
+        k = (int)(node % N);
+        run = A.st[b].status == GS_RUNNING;
+    }
+    const GSz<D> Z(N);
+    const double *x = A.x + b * Z.x() + (size_t)k * D::NX, *u = A.u + b * Z.u() + (size_t)k * D::NU;
+    const double *yi = A.yi + b * Z.i() + (size_t)k * D::NIA, *ye = A.ye + b * Z.e() + (size_t)k * D::NEA;
+    const double *lam = A.lam + b * Z.l() + (size_t)k * D::NX, *lref = A.lref + 2 * b;
+    const bool eqon = D::NE > 0 && k >= P.eq_from && k < N;
+    if (run && t < FAM::PRE) FAM::prepass(M, F, P, x, u, t, S[g]);
+    __syncthreads();
+    if (run && t == 0) FAM::seeds(P, u, yi, ye, lam, eqon, S[g]);
+    __syncthreads();
+    if (run) FAM::lane(M, F, x, u, yi, t, S[g]);
+    __syncthreads();
+    if (run) {
+        double *rec = A.rec + b * Z.rec() + (size_t)k * D::REC;
+        for (int e = t; e < D::REC; e += L) rec[e] = FAM::rec(P, x, u, yi, ye, lam, eqon, S[g], e, lref);
+    }
+}
+
+// ============================================================== initial point
+template <class FAM>
+__global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
+    using D = typename FAM::D;
+    constexpr int NX = D::NX, NU = D::NU, NI = D::NI, NIA = D::NIA, NEA = D::NEA;
+    GMODELS(FAM);
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b >= batch) return;
+    const int N = P.N;
+    const GSz<D> Z(N);
+    double *x = A.x + b * Z.x(), *u = A.u + b * Z.u(), *s = A.s + b * Z.i();
+    const double *x0 = A.x0 + (size_t)b * NX;
+    const int wst = NU + NX, wsz = NX + N * wst;
+    const double *w0 = A.w0 ? A.w0 + (size_t)b * wsz : nullptr;
+    for (int e = lane; e < (N + 1) * NX; e += 64) {
+        const int k = e / NX, j = e % NX;
+        double v = x0[j];
+        if (k > 0) v = gpush(w0 ? w0[NX + (k - 1) * wst + NU + j] : (P.init_zero ? 0.0 : x0[j]), P.x_lo[j], P.x_hi[j]);
+        x[e] = v;
+        A.zxL[b * Z.x() + e] = (k > 0 && gb(P.x_lo[j])) ? 1.0 : 0.0;
+        A.zxU[b * Z.x() + e] = (k > 0 && gb(P.x_hi[j])) ? 1.0 : 0.0;
+    }
+    for (int e = lane; e < N * NU; e += 64) {
+        const int k = e / NU, j = e % NU;
+        const double lo = A.u_lo[e], hi = A.u_hi[e];
+        const bool fixed = gb(lo) && lo == hi;
+        double v;
+        if (fixed) {
+            v = (k == 0 && A.u0) ? A.u0[(size_t)b * NU + j] : lo;
+        } else {
+            double v0 = P.has_u_init ? P.u_init[j] : (j >= P.force_from ? P.F_init : 0.0);
+            if (w0) v0 = w0[NX + k * wst + j];
+            v = gpush(v0, lo, hi);
+        }
+        u[e] = v;
+        A.zuL[b * Z.u() + e] = (!fixed && gb(lo)) ? 1.0 : 0.0;
+        A.zuU[b * Z.u() + e] = (!fixed && gb(hi)) ? 1.0 : 0.0;
+    }
+    for (int e = lane; e < N * NX; e += 64) A.lam[b * Z.l() + e] = 0.0;
+    for (int e = lane; e < N * NEA; e += 64) A.ye[b * Z.e() + e] = 0.0;
+    for (int e = lane; e < N * NIA; e += 64) A.yi[b * Z.i() + e] = 0.0;
+    gsync();
+    for (int k = lane; k < N; k += 64) {
+        double l, ci[NIA], ce[NEA], f[NX];
+        FAM::values(M, F, P, x + (size_t)k * NX, u + (size_t)k * NU, A.lref + 2 * b, l, ci, ce, f);
+        for (int r = 0; r < NI; r++) {
+            const int i = k * NIA + r;
+            const double lo = A.c_lo[k * NI + r], hi = A.c_hi[k * NI + r];
+            s[i] = gpush(ci[r], lo, hi);
+            A.vL[b * Z.i() + i] = gb(lo) ? 1.0 : 0.0;
+            A.vU[b * Z.i() + i] = gb(hi) ? 1.0 : 0.0;
+        }
+    }
+    if (lane == 0) {
+        GState st;
+        st.mu = P.mu_init; st.nu = 0.0; st.reg_last = 0.0; st.E0 = INFINITY; st.cviol = INFINITY; st.obj = 0.0;
+        st.reg_tier = 0; st.status = GS_RUNNING; st.iter = 0; st.n_ls_fail = 0; st.n_ic = 0; st.consec_fail = 0;
+        st.n_soc = 0; st.pad = 0;
+        A.st[b] = st;
+    }
+}
+
+// ============================================================== one interior-point iteration
+template <class FAM>
+__global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
+    using D = typename FAM::D;
+    constexpr int NX = D::NX, NU = D::NU, NV = D::NV, NI = D::NI, NE = D::NE, NIA = D::NIA, NEA = D::NEA;
+    constexpr int NK = NU + NEA, LDK = NK + 1;
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b >= batch) return;
+    GState st = A.st[b];
+    if (st.status != GS_RUNNING) return;
+    GMODELS(FAM);
+    __shared__ double Hs[NV * NV], Ps[NX * NX], T1[NX * NU], T2[NX * NX], Ab[NX * NX], Bb[NX * NU], Qxx[NX * NX];
+    constexpr int KSTG = NK * LDK + 2 * NK;  // per stage: factored block, perm, piv
+    constexpr int NYS = NK * (NX > 1 ? NX : 1);
+    __shared__ double Ks[NK * LDK], Ys[NYS], Rh[NK * NX], Kf[NK * NX], Jn[NEA * NX], Dds[NIA];
+    __shared__ int perm[NK], piv[NK];
+    __shared__ double vx[NV], tv[NX], zv[NK], pvs[NX], dxs[NX], dxn[NX], duv[NK];
+
+    const int N = P.N;
+    const GSz<D> Z(N);
+    double *x = A.x + b * Z.x(), *u = A.u + b * Z.u(), *s = A.s + b * Z.i(), *lam = A.lam + b * Z.l();
+    double *ye = A.ye + b * Z.e(), *yi = A.yi + b * Z.i();
+    double *zxL = A.zxL + b * Z.x(), *zxU = A.zxU + b * Z.x(), *zuL = A.zuL + b * Z.u(), *zuU = A.zuU + b * Z.u();
+    double *vL = A.vL + b * Z.i(), *vU = A.vU + b * Z.i();
+    double *dx = A.dx + b * Z.x(), *du = A.du + b * Z.u(), *ds = A.ds + b * Z.i(), *dlam = A.dlam + b * Z.l();
+    double *dye = A.dye + b * Z.e(), *dyi = A.dyi + b * Z.i();
+    double *dzxL = A.dzxL + b * Z.x(), *dzxU = A.dzxU + b * Z.x(), *dzuL = A.dzuL + b * Z.u(), *dzuU = A.dzuU + b * Z.u();
+    double *dvL = A.dvL + b * Z.i(), *dvU = A.dvU + b * Z.i();
+    double *bkp = A.bk + b * Z.bk();
+    const double *rec = A.rec + b * Z.rec();
+    double *Sx = A.Sx + b * Z.x(), *gx = A.gx + b * Z.x(), *Su = A.Su + b * Z.u(), *gu = A.gu + b * Z.u();
+    double *Ss = A.Ss + b * Z.i(), *gs = A.gs + b * Z.i();
+    double *rdyn = A.rdyn + b * Z.l(), *rin = A.rin + b * Z.i(), *req = A.req + b * Z.e();
+    double *trdyn = A.trdyn + b * Z.l(), *trin = A.trin + b * Z.i(), *treq = A.treq + b * Z.e();
+    double *sdyn = A.sdyn + b * Z.l(), *sin_ = A.sin_ + b * Z.i(), *seq = A.seq + b * Z.e();
+    double *tx = A.tx + b * Z.x(), *tu = A.tu + b * Z.u(), *ts = A.ts + b * Z.i();
+    double *Pg = A.P + b * Z.P(), *Kg = A.Kinv + b * Z.Kinv(), *Fg = A.Kfb + b * Z.Kfb(), *pvg = A.pv + b * Z.l();
+    double *kvg = A.kv + b * Z.kv();
+    const double *ulo = A.u_lo, *uhi = A.u_hi, *clo = A.c_lo, *chi = A.c_hi;
+    const double *lref = A.lref + 2 * b;
+    auto R = [&](int k) { return rec + (size_t)k * D::REC; };
+    auto ufix = [&](int i) { return gb(ulo[i]) && ulo[i] == uhi[i]; };
+    auto cact = [&](int k, int q) { return gb(clo[k * NI + q]) || gb(chi[k * NI + q]); };
+    auto eqon = [&](int k) { return NE > 0 && k >= P.eq_from && k < N; };
+    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
+    const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
+    double mu = st.mu, nu = st.nu;
+
+    auto finish = [&](int status) {
+        double f = 0.0;
+        for (int k = lane; k < N; k += 64) f += R(k)[D::O_L];
+        f = wave_sum(f);
+        if (lane == 0) {
+            st.status = status;
+            st.obj = f;
+            st.mu = mu;
+            st.nu = nu;
+            A.st[b] = st;
+            atomicSub(A.active, 1);
+        }
+    };
+
+    // ---------------- optimality error (IPOPT E_0, s_max scaling)
+    double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sm = 0, sbm = 0;
+    int nm = 0, nbm = 0;
+    auto comp = [&](double z, double gap) {
+        const double c = z * gap;
+        cinf0 = fmax(cinf0, fabs(c));
+        cinfm = fmax(cinfm, fabs(c - mu));
+        sbm += z;
+        nbm++;
+    };
+    for (int e = lane; e < N * NX; e += 64) {  // x rows, k = 1..N
+        const int k = e / NX + 1, j = e % NX, i = k * NX + j;
+        double r = -lam[(k - 1) * NX + j];
+        if (k < N) {
+            const double *rk = R(k);
+            r += rk[D::O_GL + j];
+            for (int jj = 0; jj < NX; jj++) r += rk[D::O_A + jj * NX + j] * lam[k * NX + jj];
+            for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + j] * yi[k * NIA + q];
+            if (eqon(k))
+                for (int ee = 0; ee < NE; ee++) r += rk[D::O_JE + ee * NX + j] * ye[k * NEA + ee];
+        }
+        r += -zxL[i] + zxU[i];
+        dinf = fmax(dinf, fabs(r));
+        if (gb(P.x_lo[j])) comp(zxL[i], x[i] - P.x_lo[j]);
+        if (gb(P.x_hi[j])) comp(zxU[i], P.x_hi[j] - x[i]);
+    }
+    for (int e = lane; e < N * NU; e += 64) {  // u rows (free)
+        if (ufix(e)) continue;
+        const int k = e / NU, j = e % NU;
+        const double *rk = R(k);
+        double r = rk[D::O_GL + NX + j];
+        for (int jj = 0; jj < NX; jj++) r += rk[D::O_B + jj * NU + j] * lam[k * NX + jj];
+        for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + NX + j] * yi[k * NIA + q];
+        r += -zuL[e] + zuU[e];
+        dinf = fmax(dinf, fabs(r));
+        if (gb(ulo[e])) comp(zuL[e], u[e] - ulo[e]);
+        if (gb(uhi[e])) comp(zuU[e], uhi[e] - u[e]);
+    }
+    for (int e = lane; e < N * NI; e += 64) {  // slack rows
+        const int k = e / NI, q = e % NI, i = k * NIA + q;
+        if (!cact(k, q)) continue;
+        dinf = fmax(dinf, fabs(-yi[i] - vL[i] + vU[i]));
+        if (gb(clo[e])) comp(vL[i], s[i] - clo[e]);
+        if (gb(chi[e])) comp(vU[i], chi[e] - s[i]);
+        pinf = fmax(pinf, fabs(R(k)[D::O_CI + q] - s[i]));
+        sm += fabs(yi[i]);
+        nm++;
+    }
+    for (int e = lane; e < N * NX; e += 64) {  // dynamics
+        const int k = e / NX, j = e % NX;
+        pinf = fmax(pinf, fabs(R(k)[D::O_F + j] - x[(k + 1) * NX + j]));
+        sm += fabs(lam[e]);
+        nm++;
+    }
+    if (NE > 0)
+        for (int e = lane; e < N * NE; e += 64) {
+            const int k = e / NE, ee = e % NE;
+            if (!eqon(k)) continue;
+            pinf = fmax(pinf, fabs(R(k)[D::O_CE + ee]));
+            sm += fabs(ye[k * NEA + ee]);
+            nm++;
+        }
+    dinf = wave_max(dinf); pinf = wave_max(pinf); cinf0 = wave_max(cinf0); cinfm = wave_max(cinfm);
+    sm = wave_sum(sm); sbm = wave_sum(sbm); nm = wave_sum_i(nm); nbm = wave_sum_i(nbm);
+    const double sd = fmax(s_max, (sm + sbm) / fmax(1.0, (double)(nm + nbm))) / s_max;
+    const double sc = fmax(s_max, sbm / fmax(1.0, (double)nbm)) / s_max;
+    const double E0 = fmax(fmax(dinf / sd, pinf), cinf0 / sc);
+    double Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
+    st.E0 = E0;
+    st.cviol = pinf;
+    if (E0 <= P.tol && pinf <= P.constr_viol_tol) { finish(GS_CONVERGED); return; }
+    if (st.iter >= P.max_iter) { finish(GS_MAXITER); return; }
+    while (Emu <= kappa_eps * mu && mu > P.tol / 10.0) {
+        const double mnew = fmax(P.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
+        if (mnew >= mu) break;
+        mu = mnew;
+        double cm = 0.0;
+        for (int e = lane; e < N * NX; e += 64) {
+            const int i = e + NX, j = e % NX;
+            if (gb(P.x_lo[j])) cm = fmax(cm, fabs(zxL[i] * (x[i] - P.x_lo[j]) - mu));
+            if (gb(P.x_hi[j])) cm = fmax(cm, fabs(zxU[i] * (P.x_hi[j] - x[i]) - mu));
+        }
+        for (int e = lane; e < N * NU; e += 64) {
+            if (ufix(e)) continue;
+            if (gb(ulo[e])) cm = fmax(cm, fabs(zuL[e] * (u[e] - ulo[e]) - mu));
+            if (gb(uhi[e])) cm = fmax(cm, fabs(zuU[e] * (uhi[e] - u[e]) - mu));
+        }
+        for (int e = lane; e < N * NI; e += 64) {
+            const int i = (e / NI) * NIA + e % NI;
+            if (gb(clo[e])) cm = fmax(cm, fabs(vL[i] * (s[i] - clo[e]) - mu));
+            if (gb(chi[e])) cm = fmax(cm, fabs(vU[i] * (chi[e] - s[i]) - mu));
+        }
+        cinfm = wave_max(cm);
+        Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
+    }
+    const double tau_fb = fmax(tau_min, 1.0 - mu);
+
+    // ---------------- barrier Sigma / gradients, residuals of the current point
+    for (int e = lane; e < (N + 1) * NX; e += 64) {
+        const int k = e / NX, j = e % NX;
+        double sg = 0, g = 0;
+        if (k > 0) {
+            if (gb(P.x_lo[j])) { sg += zxL[e] / (x[e] - P.x_lo[j]); g -= mu / (x[e] - P.x_lo[j]); }
+            if (gb(P.x_hi[j])) { sg += zxU[e] / (P.x_hi[j] - x[e]); g += mu / (P.x_hi[j] - x[e]); }
+        }
+        Sx[e] = sg;
+        gx[e] = g;
+    }
+    for (int e = lane; e < N * NU; e += 64) {
+        double sg = 0, g = 0;
+        if (!ufix(e)) {
+            if (gb(ulo[e])) { sg += zuL[e] / (u[e] - ulo[e]); g -= mu / (u[e] - ulo[e]); }
+            if (gb(uhi[e])) { sg += zuU[e] / (uhi[e] - u[e]); g += mu / (uhi[e] - u[e]); }
+        }
+        Su[e] = sg;
+        gu[e] = g;
+    }
+    for (int e = lane; e < N * NI; e += 64) {
+        const int k = e / NI, q = e % NI, i = k * NIA + q;
+        double sg = 0, g = 0;
+        if (gb(clo[e])) { sg += vL[i] / (s[i] - clo[e]); g -= mu / (s[i] - clo[e]); }
+        if (gb(chi[e])) { sg += vU[i] / (chi[e] - s[i]); g += mu / (chi[e] - s[i]); }
+        Ss[i] = sg;
+        gs[i] = g;
+        rin[i] = cact(k, q) ? R(k)[D::O_CI + q] - s[i] : 0.0;
+    }
+    for (int e = lane; e < N * NX; e += 64) rdyn[e] = R(e / NX)[D::O_F + e % NX] - x[(e / NX + 1) * NX + e % NX];
+    for (int e = lane; e < N * NEA; e += 64) {
+        const int k = e / NEA, ee = e % NEA;
+        req[e] = (ee < NE && eqon(k)) ? R(k)[D::O_CE + ee] : 0.0;
+    }
+    gsync();
+
+    // ---------------- Riccati factorisation with inertia test (stage blocks [[Quu, Du^T], [Du, -dc]])
+    double dw_c = 0.0, dc_c = 0.0;
+    auto factor = [&](double dw, double dc, double d1) -> int {
+        for (int e = lane; e < NX * NX; e += 64) Ps[e] = (e / NX == e % NX) ? Sx[N * NX + e / NX] + dw : 0.0;
+        __syncthreads();
+        for (int k = N - 1; k >= 0; k--) {
+            const double *rk = R(k);
+            const bool en = eqon(k + 1);
+            for (int e = lane; e < NX * NX; e += 64) {
+                Pg[(size_t)k * NX * NX + e] = Ps[e];
+                Ab[e] = rk[D::O_A + e];
+            }
+            for (int e = lane; e < NX * NU; e += 64) Bb[e] = rk[D::O_B + e];
+            for (int e = lane; e < NEA * NX; e += 64) Jn[e] = (en && e < NE * NX) ? R(k + 1)[D::O_JE + e] : 0.0;
+            for (int q = lane; q < NI; q += 64) {
+                const double sg = Ss[k * NIA + q] + dw;
+                Dds[q] = cact(k, q) ? sg / (1.0 + dc * sg) : 0.0;
+            }
+            gsync();
+            for (int e = lane; e < NV * NV; e += 64) {
+                const int a = e / NV, c = e % NV;
+                const bool fa = a < NX ? (k == 0) : ufix(k * NU + a - NX);
+                const bool fc = c < NX ? (k == 0) : ufix(k * NU + c - NX);
+                double v;
+                if (fa || fc) {
+                    v = (a == c) ? 1.0 : 0.0;
+                } else {
+                    v = rk[D::O_W + e];
+                    for (int q = 0; q < NI; q++) v += rk[D::O_JI + q * NV + a] * Dds[q] * rk[D::O_JI + q * NV + c];
+                    if (a == c) {
+                        v += dw;
+                        if (a < NX) v += Sx[k * NX + a];
+                        else {
+                            v += Su[k * NU + a - NX];
+                            if (a - NX >= P.tier1_from && a - NX < P.tier1_to) v += d1;
+                        }
+                    }
+                }
+                Hs[e] = v;
+            }
+            for (int e = lane; e < NX * NU; e += 64) {
+                const int i = e / NU, c = e % NU;
+                double acc = 0.0;
+                for (int l = 0; l < NX; l++) acc += Ps[i * NX + l] * Bb[l * NU + c];
+                T1[e] = acc;
+            }
+            for (int e = lane; e < NX * NX; e += 64) {
+                const int i = e / NX, j = e % NX;
+                double acc = 0.0;
+                for (int l = 0; l < NX; l++) acc += Ps[i * NX + l] * Ab[l * NX + j];
+                T2[e] = acc;
+            }
+            __syncthreads();
+            for (int e = lane; e < NK * NK; e += 64) {
+                const int a = e / NK, c = e % NK;
+                double v = 0.0;
+                if (a < NU && c < NU) {
+                    if (ufix(k * NU + a) || ufix(k * NU + c)) v = (a == c) ? 1.0 : 0.0;
+                    else {
+                        v = Hs[(NX + a) * NV + NX + c];
+                        for (int l = 0; l < NX; l++) v += Bb[l * NU + a] * T1[l * NU + c];
+                    }
+                } else if (a >= NU && c >= NU) {
+                    v = (a == c) ? ((en && a - NU < NE) ? -dc : -1.0) : 0.0;
+                } else {
+                    const int ee = (a >= NU ? a : c) - NU, uu = a >= NU ? c : a;
+                    if (en && ee < NE && !ufix(k * NU + uu))
+                        for (int l = 0; l < NX; l++) v += Jn[ee * NX + l] * Bb[l * NU + uu];
+                }
+                Ks[a * LDK + c] = v;
+            }
+            for (int e = lane; e < NK * NX; e += 64) {
+                const int a = e / NX, j = e % NX;
+                double v = 0.0;
+                if (k > 0) {
+                    if (a < NU) {
+                        if (!ufix(k * NU + a)) {
+                            v = Hs[(NX + a) * NV + j];
+                            for (int l = 0; l < NX; l++) v += Bb[l * NU + a] * T2[l * NX + j];
+                        }
+                    } else if (en && a - NU < NE) {
+                        for (int l = 0; l < NX; l++) v += Jn[(a - NU) * NX + l] * Ab[l * NX + j];
+                    }
+                }
+                Rh[e] = v;
+            }
+            for (int e = lane; e < NX * NX; e += 64) {
+                const int i = e / NX, j = e % NX;
+                double v = Hs[i * NV + j];
+                for (int l = 0; l < NX; l++) v += Ab[l * NX + i] * T2[l * NX + j];
+                Qxx[e] = v;
+            }
+            __syncthreads();
+            const BKInertia in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+            if (in.zero) return 2;
+            if (in.pos != NU || in.neg != NEA) return 1;
+            // the stage factorisation is kept (the solves of the vector pass and of the second-order
+            // corrections reuse it: a backward-stable LDL^T solve, not an explicit inverse)
+            double *kst = Kg + (size_t)k * KSTG;
+            for (int e = lane; e < NK * LDK; e += 64) kst[e] = Ks[e];
+            for (int e = lane; e < NK; e += 64) { kst[NK * LDK + e] = perm[e]; kst[NK * LDK + NK + e] = piv[e]; }
+            for (int e = lane; e < NK * NX; e += 64) Kf[e] = -Rh[e];
+            __syncthreads();
+            bk_solve_wave<LDK, NX>(Ks, NK, perm, piv, Kf, NX, Ys);
+            for (int e = lane; e < NK * NX; e += 64) Fg[(size_t)k * NK * NX + e] = Kf[e];
+            __syncthreads();
+            if (k > 0) {
+                for (int e = lane; e < NX * NX; e += 64) {
+                    const int i = e / NX, j = e % NX;
+                    double acc = Qxx[e];
+                    for (int a = 0; a < NK; a++) acc += Rh[a * NX + i] * Kf[a * NX + j];
+                    T2[e] = acc;
+                }
+                __syncthreads();
+                for (int e = lane; e < NX * NX; e += 64) Ps[e] = 0.5 * (T2[e] + T2[(e % NX) * NX + e / NX]);
+                __syncthreads();
+            }
+        }
+        return 0;
+    };
+
+    // ---------------- direction for constraint residuals (rd, ri, re) with the stored factorisation
+    auto direction = [&](const double *rd, const double *ri, const double *re) {
+        const double dw = dw_c, dc = dc_c;
+        for (int j = lane; j < NX; j += 64) pvs[j] = gx[N * NX + j] - lam[(N - 1) * NX + j];
+        gsync();
+        for (int k = N - 1; k >= 0; k--) {
+            const double *rk = R(k);
+            const bool en = eqon(k + 1);
+            for (int j = lane; j < NX; j += 64) pvg[k * NX + j] = pvs[j];
+            for (int a = lane; a < NV; a += 64) {
+                const bool fa = a < NX ? (k == 0) : ufix(k * NU + a - NX);
+                double g = 0.0;
+                if (!fa) {
+                    g = rk[D::O_GL + a];
+                    for (int q = 0; q < NI; q++) {
+                        const int i = k * NIA + q;
+                        double w = yi[i];
+                        if (cact(k, q)) {
+                            const double sg = Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
+                            w += Dd * (ri[i] + (gs[i] - yi[i]) / sg);
+                        }
+                        g += rk[D::O_JI + q * NV + a] * w;
+                    }
+                    if (a < NX) {
+                        g += gx[k * NX + a] - (k > 0 ? lam[(k - 1) * NX + a] : 0.0);
+                        for (int jj = 0; jj < NX; jj++) g += rk[D::O_A + jj * NX + a] * lam[k * NX + jj];
+                        if (eqon(k))
+                            for (int ee = 0; ee < NE; ee++) g += rk[D::O_JE + ee * NX + a] * ye[k * NEA + ee];
+                    } else {
+                        g += gu[k * NU + a - NX];
+                        for (int jj = 0; jj < NX; jj++) g += rk[D::O_B + jj * NU + a - NX] * lam[k * NX + jj];
+                    }
+                }
+                vx[a] = g;
+            }
+            for (int j = lane; j < NX; j += 64) {
+                double acc = pvs[j];
+                for (int l = 0; l < NX; l++) acc += Pg[(size_t)k * NX * NX + j * NX + l] * rd[k * NX + l];
+                tv[j] = acc;
+            }
+            gsync();
+            for (int a = lane; a < NK; a += 64) {
+                double z = 0.0;
+                if (a < NU) {
+                    if (!ufix(k * NU + a)) {
+                        z = vx[NX + a];
+                        for (int l = 0; l < NX; l++) z += rk[D::O_B + l * NU + a] * tv[l];
+                    }
+                } else if (en && a - NU < NE) {
+                    const int ee = a - NU;
+                    z = re[(k + 1) * NEA + ee];
+                    for (int l = 0; l < NX; l++) z += R(k + 1)[D::O_JE + ee * NX + l] * rd[k * NX + l];
+                }
+                zv[a] = z;
+            }
+            gsync();
+            {
+                const double *kst = Kg + (size_t)k * KSTG;
+                for (int e = lane; e < NK * LDK; e += 64) Ks[e] = kst[e];
+                for (int e = lane; e < NK; e += 64) {
+                    perm[e] = (int)kst[NK * LDK + e];
+                    piv[e] = (int)kst[NK * LDK + NK + e];
+                    duv[e] = -zv[e];
+                }
+                __syncthreads();
+                bk_solve_wave<LDK, 1>(Ks, NK, perm, piv, duv, 1, Ys);
+                for (int a = lane; a < NK; a += 64) kvg[k * NK + a] = duv[a];
+            }
+            if (k > 0)
+                for (int j = lane; j < NX; j += 64) {
+                    double acc = vx[j];
+                    for (int l = 0; l < NX; l++) acc += rk[D::O_A + l * NX + j] * tv[l];
+                    for (int a = 0; a < NK; a++) acc += Fg[(size_t)k * NK * NX + a * NX + j] * zv[a];
+                    dxn[j] = acc;
+                }
+            gsync();
+            for (int j = lane; j < NX; j += 64) pvs[j] = dxn[j];
+            gsync();
+        }
+        // forward sweep
+        for (int j = lane; j < NX; j += 64) { dxs[j] = 0.0; dx[j] = 0.0; }
+        for (int ee = lane; ee < NEA; ee += 64) dye[ee] = 0.0;
+        gsync();
+        for (int k = 0; k < N; k++) {
+            const double *rk = R(k);
+            const bool en = eqon(k + 1);
+            for (int a = lane; a < NK; a += 64) {
+                double acc = kvg[k * NK + a];
+                for (int j = 0; j < NX; j++) acc += Fg[(size_t)k * NK * NX + a * NX + j] * dxs[j];
+                if (a < NU && ufix(k * NU + a)) acc = 0.0;
+                duv[a] = acc;
+                if (a < NU) du[k * NU + a] = acc;
+            }
+            gsync();
+            for (int j = lane; j < NX; j += 64) {
+                double acc = rd[k * NX + j];
+                for (int l = 0; l < NX; l++) acc += rk[D::O_A + j * NX + l] * dxs[l];
+                for (int c = 0; c < NU; c++) acc += rk[D::O_B + j * NU + c] * duv[c];
+                dxn[j] = acc;
+            }
+            gsync();
+            for (int j = lane; j < NX; j += 64) {
+                double acc = pvg[k * NX + j];
+                for (int l = 0; l < NX; l++) acc += Pg[(size_t)k * NX * NX + j * NX + l] * dxn[l];
+                if (en)
+                    for (int ee = 0; ee < NE; ee++) acc += R(k + 1)[D::O_JE + ee * NX + j] * duv[NU + ee];
+                dlam[k * NX + j] = acc;
+                dx[(k + 1) * NX + j] = dxn[j];
+            }
+            if (k + 1 < N)
+                for (int ee = lane; ee < NEA; ee += 64) dye[(k + 1) * NEA + ee] = (en && ee < NE) ? duv[NU + ee] : 0.0;
+            gsync();
+            for (int j = lane; j < NX; j += 64) dxs[j] = dxn[j];
+            gsync();
+        }
+        // slack rows and bound multipliers
+        for (int e = lane; e < N * NI; e += 64) {
+            const int k = e / NI, q = e % NI, i = k * NIA + q;
+            double dyv = 0.0, dsv = 0.0;
+            if (cact(k, q)) {
+                const double *rk = R(k);
+                double jd = 0.0;
+                for (int a = 0; a < NX; a++) jd += rk[D::O_JI + q * NV + a] * dx[k * NX + a];
+                for (int a = 0; a < NU; a++) jd += rk[D::O_JI + q * NV + NX + a] * du[k * NU + a];
+                const double sg = Ss[i] + dw, Dd = sg / (1.0 + dc * sg), rs = gs[i] - yi[i];
+                dyv = Dd * (jd + ri[i] + rs / sg);
+                dsv = (dyv - rs) / sg;
+            }
+            dyi[i] = dyv;
+            ds[i] = dsv;
+        }
+        gsync();
+        for (int e = lane; e < (N + 1) * NX; e += 64) {
+            const int k = e / NX, j = e % NX;
+            double a = 0.0, c = 0.0;
+            if (k > 0) {
+                if (gb(P.x_lo[j])) a = mu / (x[e] - P.x_lo[j]) - zxL[e] - zxL[e] / (x[e] - P.x_lo[j]) * dx[e];
+                if (gb(P.x_hi[j])) c = mu / (P.x_hi[j] - x[e]) - zxU[e] + zxU[e] / (P.x_hi[j] - x[e]) * dx[e];
+            }
+            dzxL[e] = a;
+            dzxU[e] = c;
+        }
+        for (int e = lane; e < N * NU; e += 64) {
+            double a = 0.0, c = 0.0;
+            if (!ufix(e)) {
+                if (gb(ulo[e])) a = mu / (u[e] - ulo[e]) - zuL[e] - zuL[e] / (u[e] - ulo[e]) * du[e];
+                if (gb(uhi[e])) c = mu / (uhi[e] - u[e]) - zuU[e] + zuU[e] / (uhi[e] - u[e]) * du[e];
+            }
+            dzuL[e] = a;
+            dzuU[e] = c;
+        }
+        for (int e = lane; e < N * NI; e += 64) {
+            const int i = (e / NI) * NIA + e % NI;
+            double a = 0.0, c = 0.0;
+            if (gb(clo[e])) a = mu / (s[i] - clo[e]) - vL[i] - vL[i] / (s[i] - clo[e]) * ds[i];
+            if (gb(chi[e])) c = mu / (chi[e] - s[i]) - vU[i] + vU[i] / (chi[e] - s[i]) * ds[i];
+            dvL[i] = a;
+            dvU[i] = c;
+        }
+        gsync();
+    };
+
+    auto ftb = [&](double &ap_o, double &az_o) {
+        double ap = 1.0, az = 1.0;
+        auto one = [&](double v, double dv, double lo, double hi, double zl, double dzl, double zu, double dzu) {
+            if (gb(lo)) {
+                if (dv < 0) ap = fmin(ap, -tau_fb * (v - lo) / dv);
+                if (dzl < 0) az = fmin(az, -tau_fb * zl / dzl);
+            }
+            if (gb(hi)) {
+                if (dv > 0) ap = fmin(ap, tau_fb * (hi - v) / dv);
+                if (dzu < 0) az = fmin(az, -tau_fb * zu / dzu);
+            }
+        };
+        for (int e = lane + NX; e < (N + 1) * NX; e += 64) {
+            const int j = e % NX;
+            one(x[e], dx[e], P.x_lo[j], P.x_hi[j], zxL[e], dzxL[e], zxU[e], dzxU[e]);
+        }
+        for (int e = lane; e < N * NU; e += 64)
+            if (!ufix(e)) one(u[e], du[e], ulo[e], uhi[e], zuL[e], dzuL[e], zuU[e], dzuU[e]);
+        for (int e = lane; e < N * NI; e += 64) {
+            const int i = (e / NI) * NIA + e % NI;
+            one(s[i], ds[i], clo[e], chi[e], vL[i], dvL[i], vU[i], dvU[i]);
+        }
+        ap_o = wave_min(ap);
+        az_o = wave_min(az);
+    };
+
+    // barrier objective + l1 violation at (xx, uu, ss): cur = the current point (values in the records)
+    auto merit = [&](const double *xx, const double *uu, const double *ss, bool cur, double *trd, double *tri,
+                     double *tre, double &phi, double &th, bool &okp) {
+        double fs = 0.0, t = 0.0, bar = 0.0;
+        int bad = 0;
+        for (int k = lane; k < N; k += 64) {
+            double l, ci[NIA], ce[NEA], f[NX];
+            if (cur) {
+                const double *rk = R(k);
+                l = rk[D::O_L];
+                for (int q = 0; q < NI; q++) ci[q] = rk[D::O_CI + q];
+                for (int ee = 0; ee < NE; ee++) ce[ee] = rk[D::O_CE + ee];
+                for (int j = 0; j < NX; j++) f[j] = rk[D::O_F + j];
+            } else {
+                FAM::values(M, F, P, xx + (size_t)k * NX, uu + (size_t)k * NU, lref, l, ci, ce, f);
+            }
+            fs += l;
+            for (int j = 0; j < NX; j++) {
+                const double r = f[j] - xx[(k + 1) * NX + j];
+                t += fabs(r);
+                if (trd) trd[k * NX + j] = r;
+            }
+            for (int q = 0; q < NI; q++) {
+                const double r = cact(k, q) ? ci[q] - ss[k * NIA + q] : 0.0;
+                t += fabs(r);
+                if (tri) tri[k * NIA + q] = r;
+            }
+            const bool eo = eqon(k);
+            for (int ee = 0; ee < NEA; ee++) {
+                const double r = (eo && ee < NE) ? ce[ee] : 0.0;
+                t += fabs(r);
+                if (tre) tre[k * NEA + ee] = r;
+            }
+        }
+        auto blog = [&](double v, double lo, double hi) {
+            if (gb(lo)) { if (v - lo <= 0) bad = 1; else bar -= log(v - lo); }
+            if (gb(hi)) { if (hi - v <= 0) bad = 1; else bar -= log(hi - v); }
+        };
+        for (int e = lane + NX; e < (N + 1) * NX; e += 64) blog(xx[e], P.x_lo[e % NX], P.x_hi[e % NX]);
+        for (int e = lane; e < N * NU; e += 64)
+            if (!ufix(e)) blog(uu[e], ulo[e], uhi[e]);
+        for (int e = lane; e < N * NI; e += 64) blog(ss[(e / NI) * NIA + e % NI], clo[e], chi[e]);
+        fs = wave_sum(fs);
+        t = wave_sum(t);
+        bar = wave_sum(bar);
+        bad = wave_sum_i(bad);
+        phi = fs + mu * bar;
+        th = t;
+        okp = bad == 0;
+        gsync();
+    };
+    auto trial = [&](double al) {
+        for (int e = lane; e < (N + 1) * NX; e += 64) tx[e] = x[e] + al * dx[e];
+        for (int e = lane; e < N * NU; e += 64) tu[e] = u[e] + al * du[e];
+        for (int e = lane; e < N * NIA; e += 64) ts[e] = s[e] + al * ds[e];
+        gsync();
+    };
+    // direction arrays (save / restore around second-order corrections)
+    auto dir_copy = [&](bool save) {
+        double *arr[12] = {dx, du, ds, dlam, dye, dyi, dzxL, dzxU, dzuL, dzuU, dvL, dvU};
+        const size_t len[12] = {Z.x(), Z.u(), Z.i(), Z.l(), Z.e(), Z.i(), Z.x(), Z.x(), Z.u(), Z.u(), Z.i(), Z.i()};
+        size_t off = 0;
+        for (int a = 0; a < 12; a++) {
+            for (size_t e = lane; e < len[a]; e += 64) {
+                if (save) bkp[off + e] = arr[a][e];
+                else arr[a][e] = bkp[off + e];
+            }
+            off += len[a];
+        }
+        gsync();
+    };
+
+    // ---------------- inertia correction
+    double dw = 0.0, dc = 0.0, d1 = 0.0;
+    int tier = st.reg_tier, step_no = 0;
+    double reg = (st.reg_tier == 0) ? 0.0 : st.reg_last / 3.0;
+    if (st.reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
+    if (tier == 1) d1 = reg; else if (tier == 2) dw = reg;
+    const bool has_t1 = P.tier1_to > P.tier1_from;
+    bool factor_ok = false;
+    for (int tries = 0; tries < 60; tries++) {
+        const int fr = factor(dw, dc, d1);
+        if (fr == 0) { factor_ok = true; break; }
+        if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
+        st.n_ic++;
+        step_no++;
+        if (tier == 0) {
+            tier = has_t1 ? 1 : 2;
+            reg = 1e-4;
+        } else if (step_no == 1 && st.reg_tier == tier && reg < st.reg_last) {
+            reg = st.reg_last;
+        } else {
+            reg *= 8.0;
+            if (tier == 1 && reg > 1e6) { tier = 2; reg = 1e-4; }
+        }
+        if (reg > 1e40) break;
+        d1 = (tier == 1) ? reg : 0.0;
+        dw = (tier == 2) ? reg : 0.0;
+    }
+    if (!factor_ok) { finish(GS_INERTIA); return; }
+    st.reg_tier = tier;
+    st.reg_last = reg;
+    dw_c = dw;
+    dc_c = dc;
+
+    // ---------------- step, line search with second-order corrections, update
+    direction(rdyn, rin, req);
+    double ap, az;
+    ftb(ap, az);
+    double phi0, th0;
+    bool ok0;
+    merit(x, u, s, true, nullptr, nullptr, nullptr, phi0, th0, ok0);
+    double gdot = 0.0, pHp = 0.0;
+    for (int k = lane; k < N; k += 64) {
+        const double *rk = R(k);
+        for (int a = 0; a < NV; a++) {
+            const double da = a < NX ? dx[k * NX + a] : du[k * NU + a - NX];
+            gdot += rk[D::O_GL + a] * da;
+            double hd = 0.0;
+            for (int c = 0; c < NV; c++) hd += rk[D::O_W + a * NV + c] * (c < NX ? dx[k * NX + c] : du[k * NU + c - NX]);
+            pHp += da * hd;
+        }
+    }
+    for (int e = lane; e < N * NU; e += 64) { gdot += gu[e] * du[e]; pHp += Su[e] * du[e] * du[e]; }
+    for (int e = lane; e < N * NIA; e += 64) { gdot += gs[e] * ds[e]; pHp += Ss[e] * ds[e] * ds[e]; }
+    for (int e = lane + NX; e < (N + 1) * NX; e += 64) { gdot += gx[e] * dx[e]; pHp += Sx[e] * dx[e] * dx[e]; }
+    gdot = wave_sum(gdot);
+    pHp = wave_sum(pHp);
+    if (th0 > 1e-300) {
+        const double nreq = (gdot + 0.5 * fmax(pHp, 0.0)) / ((1.0 - rho) * th0);
+        if (nu < nreq) nu = nreq + 1.0;
+    }
+    const double Dphi = gdot - nu * th0, m0 = phi0 + nu * th0;
+    const double slack_m = 10.0 * 2.220446049250313e-16 * fabs(m0);
+    double alpha = ap;
+    bool accepted = false;
+    int soc_used = 0;
+    for (int ls = 0; ls < 40; ls++) {
+        trial(alpha);
+        double ph, th;
+        bool okk;
+        merit(tx, tu, ts, false, trdyn, trin, treq, ph, th, okk);
+        const double mt = ph + nu * th;
+        if (okk && isfinite(mt) && mt - m0 <= eta * alpha * fmin(Dphi, 0.0) + slack_m) { accepted = true; break; }
+        if (ls == 0 && P.max_soc > 0 && (!okk || th >= th0)) {
+            double th_old = th;
+            const double a_soc = alpha;
+            for (int e = lane; e < N * NX; e += 64) sdyn[e] = alpha * rdyn[e] + trdyn[e];
+            for (int e = lane; e < N * NIA; e += 64) sin_[e] = alpha * rin[e] + trin[e];
+            for (int e = lane; e < N * NEA; e += 64) seq[e] = alpha * req[e] + treq[e];
+            gsync();
+            for (int p = 0; p < P.max_soc; p++) {
+                dir_copy(true);
+                direction(sdyn, sin_, seq);
+                double aps, azs;
+                ftb(aps, azs);
+                trial(aps);
+                double phs, ths;
+                bool oks;
+                merit(tx, tu, ts, false, trdyn, trin, treq, phs, ths, oks);
+                const double ms = phs + nu * ths;
+                if (oks && isfinite(ms) && ms - m0 <= eta * a_soc * fmin(Dphi, 0.0) + slack_m) {
+                    accepted = true;
+                    soc_used = 1;
+                    alpha = aps;
+                    az = azs;
+                    break;
+                }
+                dir_copy(false);
+                if (!oks || ths > 0.99 * th_old) break;
+                th_old = ths;
+                for (int e = lane; e < N * NX; e += 64) sdyn[e] = aps * sdyn[e] + trdyn[e];
+                for (int e = lane; e < N * NIA; e += 64) sin_[e] = aps * sin_[e] + trin[e];
+                for (int e = lane; e < N * NEA; e += 64) seq[e] = aps * seq[e] + treq[e];
+                gsync();
+            }
+            if (accepted) break;
+        }
+        alpha *= 0.5;
+    }
+    if (!accepted) {
+        st.n_ls_fail++;
+        if (++st.consec_fail >= 5) { finish(GS_LSFAIL); return; }
+    } else {
+        st.consec_fail = 0;
+    }
+    st.n_soc += soc_used;
+    for (int e = lane; e < (N + 1) * NX; e += 64) x[e] += alpha * dx[e];
+    for (int e = lane; e < N * NU; e += 64) u[e] += alpha * du[e];
+    for (int e = lane; e < N * NIA; e += 64) { s[e] += alpha * ds[e]; yi[e] += alpha * dyi[e]; }
+    for (int e = lane; e < N * NX; e += 64) lam[e] += alpha * dlam[e];
+    for (int e = lane; e < N * NEA; e += 64) ye[e] += alpha * dye[e];
+    gsync();
+    auto zupd = [&](double &z, double dz, double sl) {
+        const double zz = z + az * dz;
+        z = fmax(fmin(zz, kappa_sigma * mu / sl), mu / (kappa_sigma * sl));
+    };
+    for (int e = lane + NX; e < (N + 1) * NX; e += 64) {
+        const int j = e % NX;
+        if (gb(P.x_lo[j])) zupd(zxL[e], dzxL[e], x[e] - P.x_lo[j]);
+        if (gb(P.x_hi[j])) zupd(zxU[e], dzxU[e], P.x_hi[j] - x[e]);
+    }
+    for (int e = lane; e < N * NU; e += 64) {
+        if (ufix(e)) continue;
+        if (gb(ulo[e])) zupd(zuL[e], dzuL[e], u[e] - ulo[e]);
+        if (gb(uhi[e])) zupd(zuU[e], dzuU[e], uhi[e] - u[e]);
+    }
+    for (int e = lane; e < N * NI; e += 64) {
+        const int i = (e / NI) * NIA + e % NI;
+        if (gb(clo[e])) zupd(vL[i], dvL[i], s[i] - clo[e]);
+        if (gb(chi[e])) zupd(vU[i], dvU[i], chi[e] - s[i]);
+    }
+    if (lane == 0) {
+        st.iter++;
+        st.mu = mu;
+        st.nu = nu;
+        A.st[b] = st;
+    }
+}
+
+// ============================================================== outputs
+template <class D>
+__global__ void k_gout(GArrays A, int N, int batch, double *w, int *status, int *iters, double *kkt, double *obj) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b >= batch) return;
+    const GSz<D> Z(N);
+    constexpr int NX = D::NX, NU = D::NU;
+    const int ws = NX + N * (NU + NX);
+    const double *x = A.x + b * Z.x(), *u = A.u + b * Z.u();
+    double *wb = w + (size_t)b * ws;
+    for (int e = lane; e < ws; e += blockDim.x) {
+        double v;
+        if (e < NX) v = x[e];
+        else {
+            const int k = (e - NX) / (NU + NX), r = (e - NX) % (NU + NX);
+            v = r < NU ? u[k * NU + r] : x[(k + 1) * NX + r - NU];
+        }
+        wb[e] = v;
+    }
+    if (lane == 0) {
+        const GState st = A.st[b];
+        if (status) status[b] = st.status;
+        if (iters) iters[b] = st.iter;
+        if (kkt) kkt[b] = st.E0;
+        if (obj) obj[b] = st.obj;
+    }
+}
+
+// single node record for tests (batch of one node, multipliers given)
+template <class FAM>
+__global__ __launch_bounds__(256) void k_grec(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                              const DevFrame *F1, GParams P, const double *xu, const double *yi,
+                                              const double *ye, const double *lam, const double *lref, double *out) {
+    using D = typename FAM::D;
+    GMODELS(FAM);
+    __shared__ typename FAM::Scratch S;
+    const int t = threadIdx.x;
+    const double *x = xu, *u = xu + D::NX;
+    if (t < FAM::PRE) FAM::prepass(M, F, P, x, u, t, S);
+    __syncthreads();
+    if (t == 0) FAM::seeds(P, u, yi, ye, lam, true, S);
+    __syncthreads();
+    if (t < FAM::LANES) FAM::lane(M, F, x, u, yi, t, S);
+    __syncthreads();
+    for (int e = t; e < D::REC; e += blockDim.x) out[e] = FAM::rec(P, x, u, yi, ye, lam, true, S, e, lref);
+}
+
+}  // namespace mf
+
+// ====================================================================== host side / C ABI
+using namespace mf;
+
+#define GHIPCHK(x)                                                                                    \
+    do {                                                                                              \
+        hipError_t e_ = (x);                                                                          \
+        if (e_ != hipSuccess) return capi_fail(MF_ERR_DEVICE, std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+    } while (0)
+
+// the kernel instantiations (family, dims) and their dispatch
+enum GKind { GK_BOX = 0, GK_CH6F = 1, GK_CH6FT = 2, GK_CH3 = 3, GK_CH3T = 4 };
+using FamBox = BoxFam;
+using FamCh6F = ChainFam<6, 1, 2, false>;
+using FamCh6FT = ChainFam<6, 1, 2, true>;
+using FamCh3 = ChainFam<3, 0, 0, false>;
+using FamCh3T = ChainFam<3, 0, 0, true>;
+
+struct mf_gproblem {
+    mf_model *m0 = nullptr, *m1 = nullptr;
+    mf_gspec spec;
+    int kind = 0, nx = 0, nu = 0, ni = 0, ne = 0;
+    GParams P;
+    std::vector<double> ulo, uhi, clo, chi;
+    const DevModel *dM0 = nullptr, *dM1 = nullptr;
+    DevFrame *dF0 = nullptr, *dF1 = nullptr;
+    double *d_ulo = nullptr, *d_uhi = nullptr, *d_clo = nullptr, *d_chi = nullptr;
+    int cap = 0;
+    std::vector<double *> bufs;
+    GArrays A;
+    GState *d_st = nullptr;
+    int *d_active = nullptr;
+};
+
+template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **, size_t>> &items, GArrays &A) {
+    using D = typename FAM::D;
+    const GSz<D> Z(N);
+    items = {{&A.x, Z.x()},    {&A.u, Z.u()},    {&A.s, Z.i()},    {&A.lam, Z.l()},  {&A.ye, Z.e()},
+             {&A.yi, Z.i()},   {&A.zxL, Z.x()},  {&A.zxU, Z.x()},  {&A.zuL, Z.u()},  {&A.zuU, Z.u()},
+             {&A.vL, Z.i()},   {&A.vU, Z.i()},   {&A.dx, Z.x()},   {&A.du, Z.u()},   {&A.ds, Z.i()},
+             {&A.dlam, Z.l()}, {&A.dye, Z.e()},  {&A.dyi, Z.i()},  {&A.dzxL, Z.x()}, {&A.dzxU, Z.x()},
+             {&A.dzuL, Z.u()}, {&A.dzuU, Z.u()}, {&A.dvL, Z.i()},  {&A.dvU, Z.i()},  {&A.bk, Z.bk()},
+             {&A.rec, Z.rec()}, {&A.Sx, Z.x()},  {&A.gx, Z.x()},   {&A.Su, Z.u()},   {&A.gu, Z.u()},
+             {&A.Ss, Z.i()},   {&A.gs, Z.i()},   {&A.rdyn, Z.l()}, {&A.rin, Z.i()},  {&A.req, Z.e()},
+             {&A.trdyn, Z.l()}, {&A.trin, Z.i()}, {&A.treq, Z.e()}, {&A.sdyn, Z.l()}, {&A.sin_, Z.i()},
+             {&A.seq, Z.e()},  {&A.tx, Z.x()},   {&A.tu, Z.u()},   {&A.ts, Z.i()},   {&A.P, Z.P()},
+             {&A.Kinv, Z.Kinv()}, {&A.Kfb, Z.Kfb()}, {&A.pv, Z.l()}, {&A.kv, Z.kv()}, {&A.x0, (size_t)D::NX},
+             {&A.lref, 2}};
+}
+
+static void gfree_ws(mf_gproblem *p) {
+    for (double *b : p->bufs) (void)hipFree(b);
+    p->bufs.clear();
+    if (p->d_st) (void)hipFree(p->d_st);
+    if (p->d_active) (void)hipFree(p->d_active);
+    p->d_st = nullptr;
+    p->d_active = nullptr;
+    p->cap = 0;
+}
+
+template <class FAM> static int gensure_ws(mf_gproblem *p, int batch) {
+    if (p->cap >= batch) return MF_OK;
+    gfree_ws(p);
+    std::vector<std::pair<double **, size_t>> items;
+    GArrays &A = p->A;
+    sizes_of<FAM>(p->spec.N, items, A);
+    for (auto &it : items) {
+        double *ptr = nullptr;
+        hipError_t he = hipMalloc(&ptr, it.second * (size_t)batch * sizeof(double));
+        if (he != hipSuccess) {
+            gfree_ws(p);
+            return capi_fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
+        }
+        (void)hipMemset(ptr, 0, it.second * (size_t)batch * sizeof(double));
+        p->bufs.push_back(ptr);
+        *it.first = ptr;
+    }
+    GHIPCHK(hipMalloc(&p->d_st, sizeof(GState) * (size_t)batch));
+    GHIPCHK(hipMalloc(&p->d_active, sizeof(int)));
+    A.st = p->d_st;
+    A.active = p->d_active;
+    A.u_lo = p->d_ulo;
+    A.u_hi = p->d_uhi;
+    A.c_lo = p->d_clo;
+    A.c_hi = p->d_chi;
+    p->cap = batch;
+    return MF_OK;
+}
+
+template <class FAM>
+static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const double *d_u0, const double *d_w0,
+                       const double *d_lref, const mf_gopts *o, double *d_w, int *d_status, int *d_iters,
+                       double *d_kkt, double *d_obj, hipStream_t s) {
+    using D = typename FAM::D;
+    int e = gensure_ws<FAM>(p, batch);
+    if (e) return e;
+    GParams P = p->P;
+    P.tol = o ? o->tol : 1e-8;
+    P.constr_viol_tol = o ? o->constr_viol_tol : 1e-8;
+    P.max_iter = o ? o->max_iter : 300;
+    P.mu_init = o ? o->mu_init : 0.1;
+    P.init_zero = o ? o->init_zero : 0;
+    P.F_init = o ? o->F_init : 0.0;
+    P.max_soc = o ? o->max_soc : 4;
+    P.has_u_init = (o && o->u_init) ? 1 : 0;
+    if (P.has_u_init)
+        for (int j = 0; j < D::NU; j++) P.u_init[j] = o->u_init[j];
+    GArrays A = p->A;
+    A.u0 = d_u0;
+    A.w0 = d_w0;
+    GHIPCHK(hipMemcpyAsync(A.x0, d_x0, sizeof(double) * D::NX * (size_t)batch, hipMemcpyDeviceToDevice, s));
+    if (d_lref) {
+        GHIPCHK(hipMemcpyAsync(A.lref, d_lref, sizeof(double) * 2 * (size_t)batch, hipMemcpyDeviceToDevice, s));
+    } else {
+        std::vector<double> lr(2 * (size_t)batch);
+        for (int b = 0; b < batch; b++) { lr[2 * b] = p->spec.line_ref[0]; lr[2 * b + 1] = p->spec.line_ref[1]; }
+        GHIPCHK(hipMemcpyAsync(A.lref, lr.data(), sizeof(double) * lr.size(), hipMemcpyHostToDevice, s));
+        GHIPCHK(hipStreamSynchronize(s));
+    }
+    GHIPCHK(hipMemcpyAsync(A.active, &batch, sizeof(int), hipMemcpyHostToDevice, s));
+    GHIPCHK(hipStreamSynchronize(s));
+    const DevModel *M0 = p->dM0, *M1 = p->dM1 ? p->dM1 : p->dM0;
+    const DevFrame *F0 = p->dF0, *F1 = p->dF1 ? p->dF1 : p->dF0;
+    hipLaunchKernelGGL(k_ginit<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+    GHIPCHK(hipGetLastError());
+    constexpr int NPB = 256 / FAM::LANES;
+    const int eval_blocks = (int)(((long)batch * P.N + NPB - 1) / NPB);
+    int active = batch;
+    const int chunk = 4;
+    for (int it = 0; it <= P.max_iter && active > 0; it += chunk) {
+        for (int c = 0; c < chunk; c++) {
+            hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
+            hipLaunchKernelGGL(k_giter<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+        }
+        GHIPCHK(hipGetLastError());
+        GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
+        GHIPCHK(hipStreamSynchronize(s));
+        if (o && o->verbose) fprintf(stderr, "[mf gipm] after %d iterations: %d running\n", it + chunk, active);
+    }
+    hipLaunchKernelGGL(k_gout<D>, dim3(batch), dim3(256), 0, s, A, P.N, batch, d_w, d_status, d_iters, d_kkt, d_obj);
+    GHIPCHK(hipGetLastError());
+    return MF_OK;
+}
+
+static int gdispatch_solve(mf_gproblem *p, int batch, const double *x0, const double *u0, const double *w0,
+                           const double *lref, const mf_gopts *o, double *w, int *st, int *it, double *kkt,
+                           double *obj, hipStream_t s) {
+    switch (p->kind) {
+        case GK_BOX: return gsolve_core<FamBox>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+        case GK_CH6F: return gsolve_core<FamCh6F>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+        case GK_CH6FT: return gsolve_core<FamCh6FT>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+        case GK_CH3: return gsolve_core<FamCh3>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+        case GK_CH3T: return gsolve_core<FamCh3T>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+    }
+    return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
+}
+
+template <class FAM> static void dims_of(int &nx, int &nu, int &ni, int &ne) {
+    nx = FAM::D::NX; nu = FAM::D::NU; ni = FAM::D::NI; ne = FAM::D::NE;
+}
+
+extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, const mf_gspec *spec, mf_gproblem **out) {
+    mf_model *m0 = const_cast<mf_model *>(m0c), *m1 = const_cast<mf_model *>(m1c);
+    if (!m0 || !spec || !out) return capi_fail(MF_ERR_ARG, "null argument");
+    if (spec->N < 1 || spec->h <= 0) return capi_fail(MF_ERR_ARG, "N >= 1 and h > 0 required");
+    if (!spec->u_lo || !spec->u_hi || !spec->c_lo || !spec->c_hi) return capi_fail(MF_ERR_ARG, "bounds required");
+    int e = capi_ensure_device();
+    if (e) return e;
+    const DevModel *dM0 = nullptr, *dM1 = nullptr;
+    const Model *h0 = nullptr, *h1 = nullptr;
+    if ((e = capi_model_dev(m0, &dM0, &h0))) return e;
+    int kind = -1;
+    const int n0 = (int)h0->joints.size();
+    if (spec->family == MF_FAM_BOX) {
+        if (!m1) return capi_fail(MF_ERR_ARG, "the box family needs two models");
+        if ((e = capi_model_dev(m1, &dM1, &h1))) return e;
+        if (n0 != 6 || (int)h1->joints.size() != 6) return capi_fail(MF_ERR_UNSUPPORTED, "box family: two 6-joint arms");
+        kind = GK_BOX;
+    } else if (spec->family == MF_FAM_CHAIN) {
+        const int ne = spec->use_line ? 2 : 0;
+        if (n0 == 6 && spec->nf == 1 && ne == 2) kind = spec->thermal ? GK_CH6FT : GK_CH6F;
+        else if (n0 == 3 && spec->nf == 0 && ne == 0) kind = spec->thermal ? GK_CH3T : GK_CH3;
+        else
+            return capi_fail(MF_ERR_UNSUPPORTED, "no chain instantiation for (n, nf, line) = (" + std::to_string(n0) +
+                                                     ", " + std::to_string(spec->nf) + ", " + std::to_string(ne) + ")");
+    } else {
+        return capi_fail(MF_ERR_ARG, "unknown family");
+    }
+    for (const Model *h : {h0, h1}) {
+        if (!h) continue;
+        for (size_t i = 0; i < h->joints.size(); i++)
+            if (h->joints[i].parent != (int)i - 1) return capi_fail(MF_ERR_UNSUPPORTED, "serial chains only");
+    }
+    mf_gproblem *p = new mf_gproblem();
+    p->m0 = m0;
+    p->m1 = m1;
+    p->spec = *spec;
+    p->kind = kind;
+    p->dM0 = dM0;
+    p->dM1 = dM1;
+    switch (kind) {
+        case GK_BOX: dims_of<FamBox>(p->nx, p->nu, p->ni, p->ne); break;
+        case GK_CH6F: dims_of<FamCh6F>(p->nx, p->nu, p->ni, p->ne); break;
+        case GK_CH6FT: dims_of<FamCh6FT>(p->nx, p->nu, p->ni, p->ne); break;
+        case GK_CH3: dims_of<FamCh3>(p->nx, p->nu, p->ni, p->ne); break;
+        case GK_CH3T: dims_of<FamCh3T>(p->nx, p->nu, p->ni, p->ne); break;
+    }
+    const int N = spec->N;
+    int rc = capi_frame_dev(m0, spec->frame0, &p->dF0);
+    if (!rc && m1) rc = capi_frame_dev(m1, spec->frame1, &p->dF1);
+    if (rc) { delete p; return rc; }
+    p->ulo.assign(spec->u_lo, spec->u_lo + (size_t)N * p->nu);
+    p->uhi.assign(spec->u_hi, spec->u_hi + (size_t)N * p->nu);
+    p->clo.assign(spec->c_lo, spec->c_lo + (size_t)N * p->ni);
+    p->chi.assign(spec->c_hi, spec->c_hi + (size_t)N * p->ni);
+    p->spec.u_lo = p->ulo.data(); p->spec.u_hi = p->uhi.data();
+    p->spec.c_lo = p->clo.data(); p->spec.c_hi = p->chi.data();
+    GParams &P = p->P;
+    memset(&P, 0, sizeof P);
+    P.N = N; P.h = spec->h; P.eq_from = spec->eq_from;
+    P.nf = spec->nf; P.use_line = spec->use_line; P.thermal = spec->thermal;
+    memcpy(P.fdir, spec->fdir, sizeof P.fdir);
+    P.wF = spec->wF; P.wqd = spec->wqd; P.wtau = spec->wtau; P.wT = spec->wT;
+    P.th_a = spec->th_a; P.th_b = spec->th_b; P.Ra = spec->Ra; P.Rh = spec->Rh;
+    memcpy(P.ktau, spec->ktau, sizeof P.ktau);
+    P.box_mg = spec->box_mg; P.box_L = spec->box_L; memcpy(P.box_pdes, spec->box_pdes, sizeof P.box_pdes);
+    P.w_box = spec->w_box; P.w_qdb = spec->w_qd;
+    memcpy(P.x_lo, spec->x_lo, sizeof P.x_lo);
+    memcpy(P.x_hi, spec->x_hi, sizeof P.x_hi);
+    if (kind == GK_BOX) { P.force_from = 12; P.tier1_from = P.tier1_to = 0; }
+    else {
+        P.force_from = n0;
+        const bool concave = spec->nf > 0 && spec->wF < 0;
+        P.tier1_from = concave ? n0 : 0;
+        P.tier1_to = concave ? n0 + spec->nf : 0;
+    }
+    auto up = [&](double **d, const std::vector<double> &h) -> int {
+        GHIPCHK(hipMalloc(d, h.size() * sizeof(double)));
+        GHIPCHK(hipMemcpy(*d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+        return MF_OK;
+    };
+    if ((rc = up(&p->d_ulo, p->ulo)) || (rc = up(&p->d_uhi, p->uhi)) || (rc = up(&p->d_clo, p->clo)) ||
+        (rc = up(&p->d_chi, p->chi))) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return MF_OK;
+}
+
+extern "C" void mf_gproblem_free(mf_gproblem *p) {
+    if (!p) return;
+    gfree_ws(p);
+    for (double *d : {p->d_ulo, p->d_uhi, p->d_clo, p->d_chi})
+        if (d) (void)hipFree(d);
+    delete p;
+}
+
+extern "C" int mf_gproblem_dims(const mf_gproblem *p, int *dims5) {
+    if (!p || !dims5) return capi_fail(MF_ERR_ARG, "null argument");
+    dims5[0] = p->nx; dims5[1] = p->nu; dims5[2] = p->ni; dims5[3] = p->ne;
+    dims5[4] = p->nx + p->spec.N * (p->nu + p->nx);
+    return MF_OK;
+}
+
+extern "C" int mf_gsolve_batch_dev(mf_gproblem *p, int batch, const double *x0, const double *u0, const double *w0,
+                                   const double *line_ref, const mf_gopts *opts, double *w, int *status, int *iters,
+                                   double *kkt, double *obj, void *stream) {
+    if (!p || !x0 || !w || batch < 1) return capi_fail(MF_ERR_ARG, "bad argument");
+    int e = capi_ensure_device();
+    if (e) return e;
+    return gdispatch_solve(p, batch, x0, u0, w0, line_ref, opts, w, status, iters, kkt, obj, (hipStream_t)stream);
+}
+
+namespace {
+struct GBuf {
+    double *p = nullptr;
+    ~GBuf() { if (p) (void)hipFree(p); }
+};
+int gh2d(GBuf &b, const double *h, size_t n) {
+    GHIPCHK(hipMalloc(&b.p, n * sizeof(double)));
+    GHIPCHK(hipMemcpy(b.p, h, n * sizeof(double), hipMemcpyHostToDevice));
+    return MF_OK;
+}
+int galloc(GBuf &b, size_t n) {
+    GHIPCHK(hipMalloc(&b.p, n * sizeof(double)));
+    return MF_OK;
+}
+}  // namespace
+
+extern "C" int mf_gsolve_batch(mf_gproblem *p, int batch, const double *x0, const double *u0, const double *w0,
+                               const double *line_ref, const mf_gopts *opts, double *w, int *status, int *iters,
+                               double *kkt, double *obj, int device) {
+    if (!p || !x0 || !w || batch < 1) return capi_fail(MF_ERR_ARG, "bad argument");
+    int e = capi_ensure_device();
+    if (e) return e;
+    GHIPCHK(hipSetDevice(device));
+    const int ws = p->nx + p->spec.N * (p->nu + p->nx);
+    GBuf dx0, du0, dw0, dl, dw, dk, dob;
+    int *dst = nullptr, *dit = nullptr;
+    if ((e = gh2d(dx0, x0, (size_t)p->nx * batch))) return e;
+    if (u0 && (e = gh2d(du0, u0, (size_t)p->nu * batch))) return e;
+    if (w0 && (e = gh2d(dw0, w0, (size_t)ws * batch))) return e;
+    if (line_ref && (e = gh2d(dl, line_ref, 2 * (size_t)batch))) return e;
+    if ((e = galloc(dw, (size_t)ws * batch)) || (e = galloc(dk, batch)) || (e = galloc(dob, batch))) return e;
+    GHIPCHK(hipMalloc(&dst, sizeof(int) * batch));
+    GHIPCHK(hipMalloc(&dit, sizeof(int) * batch));
+    e = gdispatch_solve(p, batch, dx0.p, du0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst, dit, dk.p, dob.p,
+                        nullptr);
+    if (!e) {
+        hipError_t he = hipDeviceSynchronize();
+        if (he != hipSuccess) e = capi_fail(MF_ERR_DEVICE, hipGetErrorString(he));
+    }
+    if (!e) {
+        (void)hipMemcpy(w, dw.p, sizeof(double) * ws * (size_t)batch, hipMemcpyDeviceToHost);
+        if (status) (void)hipMemcpy(status, dst, sizeof(int) * batch, hipMemcpyDeviceToHost);
+        if (iters) (void)hipMemcpy(iters, dit, sizeof(int) * batch, hipMemcpyDeviceToHost);
+        if (kkt) (void)hipMemcpy(kkt, dk.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
+        if (obj) (void)hipMemcpy(obj, dob.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
+    }
+    (void)hipFree(dst);
+    (void)hipFree(dit);
+    return e;
+}
+
+template <class FAM>
+static int grec_core(mf_gproblem *p, const double *xu, const double *yi, const double *ye, const double *lam,
+                     const double *lref, double *rec) {
+    using D = typename FAM::D;
+    GBuf a, b2, c, d, l, o;
+    int e;
+    if ((e = gh2d(a, xu, D::NV)) || (e = gh2d(b2, yi, D::NIA)) || (e = gh2d(l, lref, 2)) || (e = galloc(o, D::REC)))
+        return e;
+    std::vector<double> yev(D::NEA, 0.0);
+    for (int i = 0; i < D::NE; i++) yev[i] = ye[i];
+    if ((e = gh2d(c, yev.data(), D::NEA)) || (e = gh2d(d, lam, D::NX))) return e;
+    const DevModel *M1 = p->dM1 ? p->dM1 : p->dM0;
+    const DevFrame *F1 = p->dF1 ? p->dF1 : p->dF0;
+    hipLaunchKernelGGL(k_grec<FAM>, dim3(1), dim3(256), 0, 0, p->dM0, M1, p->dF0, F1, p->P, a.p, b2.p, c.p, d.p, l.p, o.p);
+    GHIPCHK(hipGetLastError());
+    GHIPCHK(hipDeviceSynchronize());
+    GHIPCHK(hipMemcpy(rec, o.p, sizeof(double) * D::REC, hipMemcpyDeviceToHost));
+    return D::REC;
+}
+
+// diagnostics: dual state of problem b, [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU | mu]
+template <class FAM> static int gdual_core(mf_gproblem *p, int b, double *out) {
+    using D = typename FAM::D;
+    const GSz<D> Z(p->spec.N);
+    const GArrays &A = p->A;
+    if (b < 0 || b >= p->cap) return capi_fail(MF_ERR_ARG, "problem index out of range");
+    double *src[] = {A.lam, A.yi, A.ye, A.zxL, A.zxU, A.zuL, A.zuU, A.vL, A.vU};
+    const size_t len[] = {Z.l(), Z.i(), Z.e(), Z.x(), Z.x(), Z.u(), Z.u(), Z.i(), Z.i()};
+    size_t off = 0;
+    GHIPCHK(hipDeviceSynchronize());
+    for (int a = 0; a < 9; a++) {
+        GHIPCHK(hipMemcpy(out + off, src[a] + (size_t)b * len[a], len[a] * sizeof(double), hipMemcpyDeviceToHost));
+        off += len[a];
+    }
+    GState st;
+    GHIPCHK(hipMemcpy(&st, A.st + b, sizeof st, hipMemcpyDeviceToHost));
+    out[off] = st.mu;
+    return (int)off + 1;
+}
+extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {
+    if (!p || !out) return capi_fail(MF_ERR_ARG, "null argument");
+    switch (p->kind) {
+        case GK_BOX: return gdual_core<FamBox>(p, b, out);
+        case GK_CH6F: return gdual_core<FamCh6F>(p, b, out);
+        case GK_CH6FT: return gdual_core<FamCh6FT>(p, b, out);
+        case GK_CH3: return gdual_core<FamCh3>(p, b, out);
+        case GK_CH3T: return gdual_core<FamCh3T>(p, b, out);
+    }
+    return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
+}
+
+extern "C" int mf_gnode_record(mf_gproblem *p, const double *xu, const double *yi, const double *ye, const double *lam,
+                               const double *line_ref, double *rec, int device) {
+    if (!p || !xu || !yi || !lam || !rec) return capi_fail(MF_ERR_ARG, "null argument");
+    int e = capi_ensure_device();
+    if (e) return e;
+    GHIPCHK(hipSetDevice(device));
+    const double zero2[2] = {p->spec.line_ref[0], p->spec.line_ref[1]};
+    const double *lr = line_ref ? line_ref : zero2;
+    const double ye0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const double *yv = ye ? ye : ye0;
+    switch (p->kind) {
+        case GK_BOX: return grec_core<FamBox>(p, xu, yi, yv, lam, lr, rec);
+        case GK_CH6F: return grec_core<FamCh6F>(p, xu, yi, yv, lam, lr, rec);
+        case GK_CH6FT: return grec_core<FamCh6FT>(p, xu, yi, yv, lam, lr, rec);
+        case GK_CH3: return grec_core<FamCh3>(p, xu, yi, yv, lam, lr, rec);
+        case GK_CH3T: return grec_core<FamCh3T>(p, xu, yi, yv, lam, lr, rec);
+    }
+    return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
+}

@@ -1,0 +1,188 @@
+"""Generic stage-structured OCPs on the MI355X: the dual-arm box (C3) and thermal fatigue (a8).
+
+Replaces the per-node transcription loops + ``nlpsol('ipopt')`` of
+``python/2_pilz_6_DOF/Box_Pilz_6DOF.py:219-456`` and of the thermal MPC
+(``python/Centauro_script/RepeatedMPCwithThermal.py:183-402`` with
+``python/Libraries/Tmodel_library.py:9-41``) by one ``mf_gproblem`` (``mf_gspec``, C ABI in
+include/mpcfatigue.h) solved for a batch of initial states by the generic device solver
+(csrc/gipm.hip).  The decision vector keeps the reference layout ``[x_0 | (u_k, x_{k+1})]``,
+which for the box is exactly the CSV row ``Box_Pilz_6DOF.py:464-466`` writes.
+
+    ocp = GOCP(problems.box_dual(N=50))
+    res = ocp.solve_box(q0[None])          # equilibrium-tolerance homotopy, then the reference problem
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .ocp import SolveResult
+from .problems import box_homotopy_tolerances, box_u_init, read_urdf
+
+INF = float("inf")
+FAM_CHAIN, FAM_BOX = 0, 1
+
+
+@dataclass
+class GBounds:
+    x_lo: np.ndarray
+    x_hi: np.ndarray
+    u_lo: np.ndarray
+    u_hi: np.ndarray
+    c_lo: np.ndarray
+    c_hi: np.ndarray
+    x0: np.ndarray
+
+
+def bounds(spec: dict, n: int) -> GBounds:
+    """Per-node bounds of a problem spec in the generic NLP form."""
+    N = spec["N"]
+    if spec.get("family") == "box":
+        tol = spec["pos_toll"]
+        c_lo = np.hstack([np.full((N, 6), -tol), np.asarray(spec["tau_lo"], float)])
+        c_hi = np.hstack([np.full((N, 6), tol), np.asarray(spec["tau_hi"], float)])
+        u_lo = np.hstack([np.tile(np.asarray(spec["qd_lo"], float), (N, 1)), np.full((N, 6), -INF)])
+        u_hi = np.hstack([np.tile(np.asarray(spec["qd_hi"], float), (N, 1)), np.full((N, 6), INF)])
+        u_lo[0, :12] = u_hi[0, :12] = np.asarray(spec["qd0"], float)
+        return GBounds(np.asarray(spec["q_lo"], float), np.asarray(spec["q_hi"], float), u_lo, u_hi, c_lo, c_hi,
+                       np.asarray(spec["q0"], float))
+    nf = spec["nf"]
+    x_lo = np.broadcast_to(np.asarray(spec["q_lo"], float), (n,))
+    x_hi = np.broadcast_to(np.asarray(spec["q_hi"], float), (n,))
+    x0 = np.asarray(spec["q0"], float)
+    if spec.get("thermal", False):
+        x_lo = np.r_[x_lo, np.full(n, spec["T_lo"])]
+        x_hi = np.r_[x_hi, np.full(n, spec["T_hi"])]
+        x0 = np.r_[x0, np.broadcast_to(np.asarray(spec["T0"], float), (n,))]
+    c_lo = np.broadcast_to(np.asarray(spec["tau_lo"], float), (N, n))
+    c_hi = np.broadcast_to(np.asarray(spec["tau_hi"], float), (N, n))
+    u_lo = np.hstack([np.tile(np.broadcast_to(np.asarray(spec["qd_lo"], float), (n,)), (N, 1)), np.full((N, nf), -INF)])
+    u_hi = np.hstack([np.tile(np.broadcast_to(np.asarray(spec["qd_hi"], float), (n,)), (N, 1)), np.full((N, nf), INF)])
+    u_lo[0, :n] = u_hi[0, :n] = np.broadcast_to(np.asarray(spec.get("qd0", 0.0), float), (n,))
+    return GBounds(np.asarray(x_lo, float), np.asarray(x_hi, float), u_lo, u_hi, c_lo, c_hi, x0)
+
+
+class GOCP:
+    """Owning handle of an ``mf_gproblem`` built from a spec of ``mpc_fatigue_amd.problems``."""
+
+    def __init__(self, spec: dict, models=None):
+        self.spec = spec
+        urdfs = spec["urdf"] if isinstance(spec["urdf"], (list, tuple)) else [spec["urdf"]]
+        self.models = models if models is not None else [_lib.Model(read_urdf(u)) for u in urdfs]
+        n = self.models[0].nq
+        box = spec.get("family") == "box"
+        g = _lib.GSpec()
+        g.family = FAM_BOX if box else FAM_CHAIN
+        g.N, g.h, g.eq_from = spec["N"], spec["h"], 2
+        g.frame0 = self.models[0].frame_id(spec["frame"])
+        g.frame1 = self.models[1].frame_id(spec["frame"]) if box else 0
+        if box:
+            g.box_mg, g.box_L, g.w_box, g.w_qd = spec["box_mg"], spec["box_L"], spec["w_box"], spec["w_qd"]
+            g.box_pdes[:] = list(spec["p_des"])
+        else:
+            g.nf, g.use_line = spec["nf"], int(spec["use_line"])
+            fd = np.zeros(9)
+            fd[:3 * spec["nf"]] = np.asarray(spec["fdir"], float).reshape(-1)
+            g.fdir[:] = list(fd)
+            g.line_ref[:] = list(spec.get("line_ref", [0.0, 0.0]))
+            g.wF, g.wqd, g.wtau, g.wT = spec["wF"], spec["wqd"], spec["wtau"], spec.get("wT", 0.0)
+            if spec.get("thermal", False):
+                g.thermal = 1
+                g.th_a, g.th_b, g.Ra, g.Rh = spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+                kt = np.zeros(_lib.MF_MAX_JOINTS)
+                kt[:n] = spec["ktau"]
+                g.ktau[:] = list(kt)
+        bd = bounds(spec, n)
+        lo = np.full(_lib.MF_GX_MAX, -INF)
+        hi = np.full(_lib.MF_GX_MAX, INF)
+        lo[:len(bd.x_lo)] = bd.x_lo
+        hi[:len(bd.x_hi)] = bd.x_hi
+        g.x_lo[:] = list(lo)
+        g.x_hi[:] = list(hi)
+        self._keep = [np.ascontiguousarray(a, dtype=np.float64) for a in (bd.u_lo, bd.u_hi, bd.c_lo, bd.c_hi)]
+        g.u_lo, g.u_hi, g.c_lo, g.c_hi = (_lib.dptr(a) for a in self._keep)
+        self.bounds = bd
+        h = C.c_void_p()
+        _lib.check(_lib.lib().mf_gproblem_create(self.models[0].handle, self.models[1].handle if box else None,
+                                                 C.byref(g), C.byref(h)))
+        self._h = h
+        d = (C.c_int * 5)()
+        _lib.check(_lib.lib().mf_gproblem_dims(h, d))
+        self.nx, self.nu, self.ni, self.ne, self.wsize = list(d)
+        self.N = spec["N"]
+        self.gspec = g
+
+    @property
+    def handle(self):
+        return self._h
+
+    def opts(self, tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, F_init=0.0,
+             u_init=None, max_soc=4, verbose=False):
+        o = _lib.GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), F_init, None, max_soc, int(verbose))
+        if u_init is not None:
+            o._u = np.ascontiguousarray(u_init, dtype=np.float64)
+            o.u_init = _lib.dptr(o._u)
+        return o
+
+    def solve(self, x0=None, u0=None, w0=None, line_ref=None, device: int = 0, **opts) -> SolveResult:
+        """Batched solve from initial states x0 (batch x nx; default the spec's)."""
+        x0 = self.bounds.x0[None] if x0 is None else x0
+        x0 = np.ascontiguousarray(np.atleast_2d(np.asarray(x0, float)))
+        B = x0.shape[0]
+        u0a = None if u0 is None else np.ascontiguousarray(np.broadcast_to(np.asarray(u0, float), (B, self.nu)))
+        w0a = None if w0 is None else np.ascontiguousarray(np.broadcast_to(np.asarray(w0, float), (B, self.wsize)))
+        lr = None if line_ref is None else np.ascontiguousarray(np.asarray(line_ref, float).reshape(B, 2))
+        o = self.opts(**opts)
+        w = np.zeros((B, self.wsize))
+        st, it = np.zeros(B, np.int32), np.zeros(B, np.int32)
+        kkt, obj = np.zeros(B), np.zeros(B)
+        _lib.check(_lib.lib().mf_gsolve_batch(self._h, B, _lib.dptr(x0), None if u0a is None else _lib.dptr(u0a),
+                                              None if w0a is None else _lib.dptr(w0a),
+                                              None if lr is None else _lib.dptr(lr), C.byref(o), _lib.dptr(w),
+                                              _lib.iptr(st), _lib.iptr(it), _lib.dptr(kkt), _lib.dptr(obj), device))
+        return SolveResult(w, st, it, kkt, obj)
+
+    def solve_dev(self, x0_ptr, u0_ptr, w0_ptr, lref_ptr, batch: int, out: dict, stream: int = 0, **opts) -> None:
+        """Device-pointer form (torch tensors' data_ptr(); u0 / w0 / lref may be None)."""
+        o = self.opts(**opts)
+        _lib.check(_lib.lib().mf_gsolve_batch_dev(self._h, batch, x0_ptr, u0_ptr, w0_ptr, lref_ptr, C.byref(o),
+                                                  out["w"], out["status"], out["iters"], out["kkt"], out["obj"],
+                                                  stream))
+
+    def node_record(self, xu, yi, ye, lam, line_ref=None, device: int = 0) -> np.ndarray:
+        """One node record from the device kernel (layout: mf_gnode_record)."""
+        arr = [np.ascontiguousarray(a, dtype=np.float64) for a in (xu, yi, ye if self.ne else np.zeros(1), lam)]
+        lr = None if line_ref is None else np.ascontiguousarray(line_ref, dtype=np.float64)
+        rec = np.zeros(8192)
+        n = _lib.check(_lib.lib().mf_gnode_record(self._h, *[_lib.dptr(a) for a in arr],
+                                                  None if lr is None else _lib.dptr(lr), _lib.dptr(rec), device))
+        return rec[:n]
+
+    def solve_box(self, q0=None, device: int = 0, tolerances=None, **opts) -> tuple[SolveResult, list]:
+        """C3 solve: the equilibrium-tolerance homotopy of problems.box_homotopy_tolerances, each
+        stage a solve warm-started from the previous stage's primal point; the last stage is the
+        reference problem itself (pos_toll = 1e-4).  Returns (last result, per-stage results)."""
+        assert self.spec.get("family") == "box"
+        stages = []
+        w = None
+        opts.setdefault("max_iter", 1000)
+        for tol in (tolerances or box_homotopy_tolerances()):
+            g = GOCP(dict(self.spec, pos_toll=tol), models=self.models)
+            r = g.solve(x0=q0, w0=w, device=device, u_init=box_u_init(self.spec), **opts)
+            stages.append(r)
+            w = r.w
+        return stages[-1], stages
+
+    def q_traj(self, w: np.ndarray) -> np.ndarray:
+        """State trajectory x_0..x_N (N+1, nx) of a solution vector."""
+        nx, nu, N = self.nx, self.nu, self.N
+        return np.vstack([w[:nx][None], w[nx:].reshape(N, nu + nx)[:, nu:]])
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib._lib is not None:
+            _lib._lib.mf_gproblem_free(h)
+            self._h = None

@@ -53,7 +53,7 @@ class GOpts(C.Structure):
     _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
                 ("mu_init", C.c_double), ("init_zero", C.c_int), ("verbose", C.c_int), ("F_init", C.c_double),
                 ("w0", C.POINTER(C.c_double)), ("bound_relax", C.c_double),
-                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int)]
+                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("dual_out", C.POINTER(C.c_double))]
 
 
 _lib = None
@@ -176,9 +176,12 @@ def w_size(g: GOCP) -> int:
 
 
 def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, verbose=0, F_init=0.0,
-         w0=None, bound_relax=0.0, u_init=None, max_soc=0):
+         w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None):
     o = GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), F_init, None, bound_relax, None,
-              max_soc)
+              max_soc, None)
+    if dual_out is not None:
+        o._d = dual_out
+        o.dual_out = _p(dual_out)
     if u_init is not None:
         o._u_init = np.ascontiguousarray(u_init, dtype=np.float64)
         o.u_init = _p(o._u_init)

@@ -80,6 +80,7 @@ typedef struct {
     double bound_relax;             /* IPOPT bound_relax_factor (0 = off) */
     const double *u_init;           /* initial control (nu) for every node, or NULL (0 / F_init) */
     int max_soc;                    /* IPOPT max_soc (second-order corrections per iteration; 0 = off) */
+    double *dual_out;               /* diagnostics: [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU | mu] or NULL */
 } mfg_opts;
 
 typedef struct {
@@ -355,8 +356,7 @@ static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
         memset(Dm, 0, sizeof(double) * mb * mb);
 #define D_(i, j) Dm[(i) * m + (j)]
         for (int j = 0; j < nx; j++) {
-            if (k > 0) {
-                D_(ol + j, ol + j) = -dc;
+            if (k > 0) {  /* dynamics rows stay unregularised (delta_c acts on c_eq and slack rows) */
                 D_(ol + j, ox + j) = D_(ox + j, ol + j) = -1.0;
             } else {
                 D_(ol + j, ol + j) = -1.0; /* lam_{-1}: dummy */
@@ -1044,6 +1044,13 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
         res->n_ls_fail = n_ls_fail; res->n_inertia_fix = n_ic;
     }
     if (O->verbose) fprintf(stderr, "second-order corrections accepted: %d\n", n_soc);
+    if (O->dual_out) {
+        double *o = O->dual_out;
+        const double *src[] = {S->lam, S->yi, S->ye, S->zxL, S->zxU, S->zuL, S->zuU, S->vL, S->vU};
+        const size_t len[] = {(size_t)N * nx, NI, NE, NX1, NX1, NU, NU, NI, NI};
+        for (int a = 0; a < 9; a++) { memcpy(o, src[a], len[a] * sizeof(double)); o += len[a]; }
+        *o = mu;
+    }
     double **pp[] = {&S->ulo, &S->uhi, &S->clo, &S->chi, &S->x, &S->u, &S->s, &S->lam, &S->ye, &S->yi, &S->zxL,
                      &S->zxU, &S->zuL, &S->zuU, &S->vL, &S->vU, &S->tx, &S->tu, &S->ts, &S->l, &S->gl, &S->ci,
                      &S->Ji, &S->ce, &S->Je, &S->f, &S->Af, &S->Bf, &S->W, &S->dx, &S->du, &S->ds, &S->dlam,

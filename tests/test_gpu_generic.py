@@ -1,0 +1,109 @@
+"""GPU parity of the generic solver (csrc/gipm.hip, C ABI mf_gproblem_* / mf_gsolve_batch) against the
+generic oracle (oracle/mf_ocp.c) and against the reference's own IPOPT trajectories.
+
+* node records of the device kernel = the oracle's hyper-dual records (box, chain, thermal)
+* C2 through the generic path = the generic oracle (same iteration, same options)
+* C3 Box_Pilz_6DOF.py re-solved on the GPU from the reference's IK start matches plotter/solution.csv
+  (G1, N=50), Result_2 (G2, N=80) and Result_1 (G4) to 1e-6 rad on every joint angle (SURVEY.md
+  s.8c (vi)), and equals the oracle's solve
+* the thermal C2 variant (a8) = the oracle
+"""
+import numpy as np
+import pytest
+
+from mpc_fatigue_amd import problems as PR
+from oracle import generic as G
+from tests.conftest import has_gpu
+
+pytestmark = pytest.mark.gpu
+
+if has_gpu():
+    from mpc_fatigue_amd.gocp import GOCP
+
+
+def rec_split(rec, nx, nu, ni, ne):
+    nv = nx + nu
+    o = [0]
+
+    def take(n, shape=None):
+        a = rec[o[0]:o[0] + n]
+        o[0] += n
+        return a.reshape(shape) if shape else a
+    l = take(1)[0]
+    gl = take(nv)
+    ci = take(ni)
+    Ji = take(ni * nv, (ni, nv))
+    ce = take(ne)
+    Je = take(ne * nx, (ne, nx))
+    f = take(nx)
+    A = take(nx * nx, (nx, nx))
+    B = take(nx * nu, (nx, nu))
+    W = take(nv * nv, (nv, nv))
+    return l, gl, ci, Ji, ce, Je, f, A, B, W
+
+
+@pytest.mark.parametrize("case", ["chain", "thermal", "box"])
+def test_device_node_record_matches_oracle(golden, case):
+    rng = np.random.default_rng(7)
+    if case == "box":
+        g, _ = golden["G1_box_N50"]
+        spec = PR.box_dual(N=2)
+        xu = g[20 * 30:21 * 30].copy()
+    elif case == "chain":
+        spec = dict(PR.pilz6_bench(N=2), wtau=0.2)
+        xu = np.r_[rng.normal(size=6), 0.3 * rng.normal(size=6), [15.0]]
+    else:
+        spec = PR.pilz6_thermal(N=2)
+        xu = np.r_[rng.normal(size=6), 60 + rng.normal(size=6), 0.3 * rng.normal(size=6), [25.0]]
+    ocp = GOCP(spec)
+    nx, nu, ni, ne = ocp.nx, ocp.nu, ocp.ni, ocp.ne
+    yi, ye, lam = 10 * rng.normal(size=ni), rng.normal(size=max(ne, 1)), rng.normal(size=nx)
+    rec = ocp.node_record(xu, yi, ye, lam, line_ref=spec.get("line_ref"))
+    l, gl, ci, Ji, ce, Je, f, A, B, W = rec_split(rec, nx, nu, ni, ne)
+    vals, jac, H = G.node_derivs(spec, xu, yi, ye, lam)
+    sc = lambda a: max(1.0, np.abs(a).max())
+    assert abs(l - vals[0]) <= 1e-12 * sc(vals[0])
+    np.testing.assert_allclose(ci, vals[1:1 + ni], atol=1e-11 * sc(ci))
+    np.testing.assert_allclose(f, vals[1 + ni + ne:], atol=1e-12 * sc(f))
+    np.testing.assert_allclose(gl, jac[0], atol=1e-11 * sc(gl))
+    np.testing.assert_allclose(Ji, jac[1:1 + ni], atol=1e-11 * sc(Ji))
+    np.testing.assert_allclose(Je, jac[1 + ni:1 + ni + ne, :nx], atol=1e-12 * sc(Je))
+    np.testing.assert_allclose(A, jac[1 + ni + ne:, :nx], atol=1e-12 * sc(A))
+    np.testing.assert_allclose(B, jac[1 + ni + ne:, nx:], atol=1e-12 * sc(B))
+    np.testing.assert_allclose(W, H, atol=1e-10 * sc(H))
+
+
+def test_c2_generic_path_matches_oracle():
+    spec = PR.pilz6_bench(N=20)
+    ocp = GOCP(spec)
+    r = ocp.solve(F_init=PR.BENCH_F_INIT, max_soc=4)
+    w_ref, r_ref = G.solve(spec, F_init=PR.BENCH_F_INIT, max_iter=300, max_soc=4)
+    assert r.status[0] == 0 and r_ref.status == 0
+    assert abs(int(r.iters[0]) - r_ref.iter) <= 2
+    np.testing.assert_allclose(r.w[0], w_ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("name,kw", [("G1_box_N50", dict(N=50)), ("G2_box_N80", dict(N=80)),
+                                     ("G4_box_N80", dict(N=80, right_const=False))])
+def test_box_gpu_resolve_matches_reference(golden, name, kw):
+    g, N = golden[name]
+    spec = PR.box_dual(q0=g[:12], **kw)
+    ocp = GOCP(spec)
+    r, stages = ocp.solve_box()
+    assert all(int(s.status[0]) == 0 for s in stages), [(int(s.status[0]), int(s.iters[0])) for s in stages]
+    dq = np.abs(ocp.q_traj(r.w[0]) - ocp.q_traj(g)).max()
+    assert dq < 1e-6, dq
+    # and the device solve equals the oracle's solve of the same homotopy
+    w_or = None
+    for tol in PR.box_homotopy_tolerances():
+        w_or, ro = G.solve(dict(spec, pos_toll=tol), w0=w_or, u_init=PR.box_u_init(spec), max_iter=1000, max_soc=4)
+    assert np.abs(ocp.q_traj(r.w[0]) - ocp.q_traj(w_or)).max() < 1e-7
+
+
+def test_thermal_gpu_matches_oracle():
+    spec = PR.pilz6_thermal(N=40, T0=79.0)
+    ocp = GOCP(spec)
+    r = ocp.solve(F_init=PR.BENCH_F_INIT, max_soc=4)
+    w_ref, r_ref = G.solve(spec, F_init=PR.BENCH_F_INIT, max_iter=300, max_soc=4)
+    assert r.status[0] == 0 and r_ref.status == 0
+    np.testing.assert_allclose(r.w[0], w_ref, atol=1e-6)

@@ -197,3 +197,37 @@ def test_unroll_torques_match_oracle():
                  - O.jacobian(ref, u["q"][k], "prbt_link_5").T @ np.r_[u["F"][k, 0], 0, 0, 0, 0, 0])
         np.testing.assert_allclose(u["tau"][k], t_ref, atol=1e-9)
         assert np.all(u["tau"][k] <= sp["tau_hi"][k] + 1e-6) and np.all(u["tau"][k] >= sp["tau_lo"][k] - 1e-6)
+
+
+def test_headline_config_c2_n100_matches_oracle():
+    """The benchmark instance itself (C5 horizons at N = 100, bench.py's batch, seed 0): 64 horizons
+    solved on the GPU equal the oracle's solves (q 1e-6 rad, same status, iterations +-2)."""
+    N, B = 100, 64
+    base = PR.pilz6_bench(N=N)
+    ocp = OCP(base)
+    ref = load_urdf_file(PR.urdf_path(base["urdf"]))
+    Q0 = PR.pilz6_batch_q0(B, seed=0)
+    LR = np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in Q0])
+    res = ocp.solve(Q0, line_ref=LR, F_init=PR.BENCH_F_INIT, tol=1e-8, constr_viol_tol=1e-8, max_iter=300)
+    specs = [PR.pilz6_bench(N=N, q0=Q0[b], line_ref=LR[b]) for b in range(B)]
+    W, R = O.solve_batch(ref, specs, F_init=PR.BENCH_F_INIT, tol=1e-8, constr_viol_tol=1e-8, max_iter=300)
+    worst = 0.0
+    for b in range(B):
+        assert R[b].status == res.status[b] == 0, (b, R[b].status, res.status[b])
+        q_gpu, _, _ = ocp.unpack(res.w[b])
+        q_ref, _, _ = ocp.unpack(W[b])
+        worst = max(worst, np.abs(q_gpu - q_ref).max())
+        assert abs(int(res.iters[b]) - R[b].iter) <= 2, (b, res.iters[b], R[b].iter)
+    assert worst <= 1e-6, worst
+
+
+def test_reference_15nm_floor_same_nonconverged_status():
+    """C2 exactly as force_optimization_pilz_6DOF.py states it (fatigue floor 15 Nm, L84-89) has no
+    feasible point: GPU and oracle both stop at max_iter, infeasible."""
+    spec = PR.pilz6_force(N=100)
+    ocp = OCP(spec)
+    ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
+    res = ocp.solve(np.array(spec["q0"])[None], F_init=PR.BENCH_F_INIT, max_iter=200)
+    _, r = O.solve(ref, spec, F_init=PR.BENCH_F_INIT, max_iter=200)
+    assert r.status == 1 and int(res.status[0]) == 1
+    assert r.cviol > 1.0 and res.kkt[0] > 1.0
