@@ -12,10 +12,15 @@ all ranks / max-over-ranks wall time (inputs resident in HBM).
     python bench.py [--gpus N --steps K --warmup W --batch B --nodes 100]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Also reported: the dominant kernel's achieved rate against its roofline
-(per-kernel HIP-event timing over the timed region, algorithmic bytes from
-DESIGN.md section 5), and the CPU baseline = the oracle's C restatement of the
-same solver on the host cores (rank 0, N = 1 only, bounded sample).
+Also reported: the node-evaluation kernel's achieved rate against its HBM
+roofline (per-kernel HIP-event timing over the timed region, SURVEY.md s.8(d)'s
+952 algorithmic bytes per node evaluation, PMC traffic per node evaluation from
+profiles/pmc_traffic.json), the iteration tail (GPU time per 4-iteration chunk
+and running count), C5's 1024-horizon shard and the single-problem latency, and
+the CPU baseline = the same interior-point algorithm on the host with the
+product's node functions compiled for the CPU, on all cores and on one core
+(rank 0, N = 1 only, bounded sample), whose solutions are compared with the
+GPU's for the same horizons (max_dq).
 """
 from __future__ import annotations
 
@@ -35,22 +40,45 @@ HBM_PEAK_GBS = 8000.0         # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-lev
 FP64_PEAK_TFS = 78.6          # MI355X FP64 vector peak (spec)
 
 
-def node_bytes(n: int, nf: int, nl: int) -> dict:
-    """Algorithmic HBM bytes per shooting node of one running horizon per launch.
+# algorithmic bytes of the C2 node evaluation, per shooting node.  Read q_k(6),
+# qd_k(6), F_k(1) = 104 B; write x_next(6) + cost(1) + tau(6) + line(2) + d tau/d(q,qd,F) (78)
+# + d line/dq (12) + d cost/dF (1) = 106 doubles = 848 B.
+NODE_BYTES = 952
 
-    k_eval_node: reads q, qd, F, y_tau, y_line of the node; writes d tau/dw (n x nv), the raw
-                 Hessian columns of the 2n lane directions (nv x 2n), d line/dq, tau, line, cost
-    k_eval_asm : reads the raw Hessian's lower triangle, d tau/dw, the torque-slack and bound
-                 multiplier data of the node; writes the condensed stage Hessian H0 and grad f
-    k_ipm_kkt  : reads H0, d tau/dw, grad f and the stage data once, writes and reads back the
-                 Riccati slot (Ku, Kl, P_{k+1}, ku, kl, p_{k+1}) and the step
-    """
-    nv, nu, nla = 2 * n + nf, n + nf, max(nl, 1)
-    ev = (2 * n + nf + n + nl) + (n * nv + nv * 2 * n + nl * n + n + nl + 1)
-    asm = (nv * (nv + 1) // 2 + n * nv + 3 * n + 2 * n + 6 * n + n + nf) + (nv * nv + nv)
-    slot = nu * n + nl * n + n * n + nu + nl + n
-    kkt = (nv * nv + n * nv + nv + n + nla + nl * n) + 2 * slot + (2 * n + nf + n + nl + n) + (2 * n + nv + 2 * n + nla)
-    return {"k_eval_node": 8 * ev, "k_eval_asm": 8 * asm, "k_ipm_kkt": 8 * kkt}
+
+def cpu_baseline(spec_of, Q0, lrefs, opts, threads: int, sample_mt: int, sample_1t: int, reps: int):
+    """The CPU baseline (rank 0, N = 1): the same interior-point algorithm on the host -- the generic
+    oracle IPM (oracle/mf_ocp.c) with the product's forward-over-reverse node functions compiled for
+    the host (oracle/cpu_fast.cpp, -O3 AVX2/FMA) -- OpenMP over horizons on `threads` cores and on one
+    core; median of `reps` timed runs after one warm-up run.  Returns (record, CPU solutions)."""
+    from oracle import cpu_fast as CF
+
+    specs = [spec_of(Q0[i], lrefs[i]) for i in range(max(sample_mt, sample_1t))]
+    kw = dict(opts, **CF.FastNodes(specs[0]).opts_kw())
+
+    def run(sp, nt):
+        t0 = time.perf_counter()
+        w, R = CF.solve_batch(sp, nthreads=nt, **kw)
+        return time.perf_counter() - t0, w, R
+
+    out = {}
+    for label, S, nt in (("all_cores", sample_mt, threads), ("one_core", sample_1t, 1)):
+        run(specs[:min(S, nt)], nt)  # warm-up
+        ts = []
+        for _ in range(reps):
+            dt, w, R = run(specs[:S], nt)
+            ts.append(dt)
+        conv = sum(1 for r in R if r.status == 0)
+        out[label] = {"value": conv / float(np.median(ts)), "threads": nt, "horizons": S, "converged": conv,
+                      "median_s": float(np.median(ts)), "runs_s": [round(t, 3) for t in ts]}
+        if label == "all_cores":
+            w_mt, st_mt = w, np.array([r.status for r in R])
+    rec = {"value": out["all_cores"]["value"], "unit": "horizons/s", "cores": threads, "kind": "port",
+           "single_core": out["one_core"]["value"], "nproc": os.cpu_count(), "detail": out,
+           "sample": (f"first {sample_mt} horizons of the same batch on {threads} threads and the first {sample_1t} "
+                      f"on 1 thread (median of {reps} runs after a warm-up); generic IPM oracle/mf_ocp.c with the "
+                      "product's node functions, both built for the host at -O3 -march=x86-64-v3 (oracle/libmfcpu.so)")}
+    return rec, w_mt, st_mt
 
 
 def main() -> int:
@@ -63,7 +91,9 @@ def main() -> int:
     ap.add_argument("--nodes", type=int, default=100)
     ap.add_argument("--max-iter", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=0, help="horizons in the CPU sample (0: 2 per thread)")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="horizons in the CPU sample (0: 4 per thread)")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU runs (median reported)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the 1024-shard and single-problem figures")
     args = ap.parse_args()
 
     import torch
@@ -137,41 +167,50 @@ def main() -> int:
     converged = float(conv.item())
     value = converged * args.steps / elapsed
 
-    # ---- dominant kernel vs roofline (this rank's HIP-event timing over the timed region)
+    # ---- node-evaluation kernel vs its HBM roofline; HIP events on the solve stream
     stats = ocp.kernel_stats()
+    trace = ocp.trace()
     ocp.timing(False)
-    nb = node_bytes(n, ocp.nf, ocp.nl)
-    dom = max(stats, key=lambda k: stats[k][0])
-    dom_ms, dom_launches = stats[dom]
-    per_launch_ms = dom_ms / max(1, dom_launches)
-    if dom in nb:
-        total_bytes = nb[dom] * float(node_evals.item()) * args.steps
-        achieved = total_bytes / (dom_ms / 1e3) / 1e9
-        bytes_per_launch = total_bytes / max(1, dom_launches)
-    else:
-        achieved, bytes_per_launch = None, None
+    ev_ms, ev_launches = stats["k_eval_node"]
+    per_launch_ms = ev_ms / max(1, ev_launches)
+    total_bytes = NODE_BYTES * float(node_evals.item()) * args.steps  # this rank's node evaluations
+    bytes_per_launch = total_bytes / max(1, ev_launches)
+    achieved = total_bytes / (ev_ms / 1e3) / 1e9
     traffic, fp64 = None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
-            pmc = json.load(f).get(dom, {})
-        traffic = pmc.get("hbm_bytes_per_launch")
-        if pmc.get("fp64_flops_per_launch"):
-            # executed FP64 flops per launch (PMC, same workload) over this run's launch time
-            tfs = pmc["fp64_flops_per_launch"] / (per_launch_ms / 1e3) / 1e12
+            pmc = json.load(f)
+        ev = pmc.get("k_eval_node", {})
+        if ev.get("hbm_bytes_per_node_eval"):
+            traffic = ev["hbm_bytes_per_node_eval"] * total_bytes / NODE_BYTES / max(1, ev_launches)
+        if ev.get("fp64_flops_per_node_eval"):
+            fl = ev["fp64_flops_per_node_eval"] * total_bytes / NODE_BYTES / max(1, ev_launches)
+            tfs = fl / (per_launch_ms / 1e3) / 1e12
             fp64 = {"achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfs / FP64_PEAK_TFS,
-                    "flops_per_launch": pmc["fp64_flops_per_launch"],
-                    "note": "FP64 VALU work (the bound of this kernel); flops from SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 x 64 lanes"}
+                    "flops_per_launch": fl,
+                    "note": "executed FP64 VALU flops (PMC SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 x 64, per node evaluation "
+                            "of the same workload, profiles/pmc_traffic.json) over this run's launch time"}
+    total_ms = sum(v[0] for v in stats.values())
     roofline = {
-        "kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-        "avg_launch_ms": per_launch_ms, "launches": dom_launches, "algorithmic_bytes_per_launch": bytes_per_launch,
-        "kernel_ms": {k: v[0] for k, v in stats.items()}, "fp64": fp64,
+        "kernel": "k_eval_node", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "traffic_over_algorithmic": (traffic / bytes_per_launch) if traffic else None,
+        "algorithmic_bytes_per_launch": bytes_per_launch, "bytes_per_node": NODE_BYTES,
+        "avg_launch_ms": per_launch_ms, "launches": ev_launches,
+        "kernel_ms": {k: v[0] for k, v in stats.items()},
+        "kernel_share": {k: v[0] / total_ms for k, v in stats.items()}, "fp64": fp64,
+        "launch_note": ("one k_eval_node launch = the solver's phase 0: k_eval_node<..,0> (q directions) then "
+                        "k_eval_node<..,1> (qd directions) on one stream; rocprofv3 lists the two, their averages "
+                        "sum to avg_launch_ms. Bytes: SURVEY.md s.8(d) 952 B per running node evaluation"),
     }
-    if dom == "k_eval_node":
-        roofline["launch_note"] = ("one k_eval_node launch = the solver's phase 0: k_eval_node<..,0> (q directions) "
-                                   "then k_eval_node<..,1> (qd directions) on one stream; rocprofv3 lists the two, "
-                                   "their averages sum to avg_launch_ms")
+    # iteration tail: per 4-iteration chunk, problems running at its start and its GPU time (last step)
+    tr_ms = trace["ms"]
+    tail = trace["running"] < 0.1 * B
+    tail_rec = {"chunks": len(tr_ms), "gpu_ms": float(tr_ms.sum()), "share_below_10pct_running":
+                float(tr_ms[tail].sum() / max(tr_ms.sum(), 1e-12)),
+                "running_at_chunk": [int(x) for x in trace["running"]],
+                "ms_per_chunk": [round(float(x), 2) for x in tr_ms]}
 
     result = {
         "metric": METRIC, "value": value, "unit": "horizons/s", "n_gpus": world, "steps": args.steps,
@@ -185,28 +224,53 @@ def main() -> int:
                    "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
                    "tol": opts["tol"]},
         "roofline": roofline,
+        "tail": tail_rec,
         "cpu_baseline": None,
     }
 
+    if world == 1 and not args.no_extra:
+        # C5's per-GPU shard (1024 horizons) and the single-problem latency (BASELINE config 2), same solver
+        def timed(nb, reps):
+            o = {k: v[:nb] for k, v in out.items()}
+            pt = {k: v.data_ptr() for k, v in o.items()}
+            ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=stream.cuda_stream, **opts)
+            ts = []
+            for _ in range(reps):
+                torch.cuda.synchronize(dev)
+                t = time.perf_counter()
+                ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=stream.cuda_stream, **opts)
+                torch.cuda.synchronize(dev)
+                ts.append(time.perf_counter() - t)
+            return float(np.median(ts)), int((o["status"] == 0).sum().item())
+        if B >= 1024:
+            t1024, c1024 = timed(1024, 3)
+            result["c5_shard_1024"] = {"value": c1024 / t1024, "unit": "horizons/s", "ms_per_step": t1024 * 1e3,
+                                       "converged": c1024, "note": "first 1024 horizons of the batch, median of 3"}
+        t1, c1 = timed(1, 5)
+        result["single_problem"] = {"ms_per_solve": t1 * 1e3, "converged": c1, "iters": int(out["iters"][0].item()),
+                                    "note": "horizon 0 of the batch alone, median of 5 (host-polled every 4 iterations)"}
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        from oracle import oracle as O
         from oracle import pin_np as P
         from oracle.urdf_np import load_urdf_file
 
         threads = min(16, os.cpu_count() or 1)
-        S = args.cpu_sample or 2 * threads
+        S = args.cpu_sample or 4 * threads
         ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
         Qs = Q0_all[:S]
-        specs = [PR.pilz6_bench(N=N, q0=Qs[i], line_ref=P.forward_kinematics(ref, Qs[i], "prbt_link_5")[0][:2])
-                 for i in range(S)]
-        c0 = time.perf_counter()
-        _, R = O.solve_batch(ref, specs, nthreads=threads, **opts)
-        c1 = time.perf_counter()
-        cconv = sum(1 for r in R if r.status == 0)
-        result["cpu_baseline"] = {"value": cconv / (c1 - c0), "unit": "horizons/s", "cores": threads,
-                                  "kind": "port",
-                                  "sample": f"first {S} horizons of the same batch, oracle/mf_oracle.c IPM, "
-                                            f"OpenMP over horizons, {cconv}/{S} converged, {c1 - c0:.1f} s"}
+        lrs = [P.forward_kinematics(ref, Qs[i], "prbt_link_5")[0][:2] for i in range(S)]
+        rec, w_cpu, st_cpu = cpu_baseline(lambda q, lr: PR.pilz6_bench(N=N, q0=q, line_ref=lr), Qs, lrs, opts,
+                                          threads, S, max(2, min(8, S)), args.cpu_reps)
+        # the bench's own answers against the CPU solutions of the same horizons
+        w_gpu = out["w"][:S].cpu().numpy()
+        st_gpu = out["status"][:S].cpu().numpy()
+        both = (st_gpu == 0) & (st_cpu == 0)
+        wq = lambda w: np.concatenate([w[:, :n]] + [w[:, n + k * (2 * n + ocp.nf) + n + ocp.nf:
+                                                       n + (k + 1) * (2 * n + ocp.nf)] for k in range(N)], axis=1)
+        rec["gpu_vs_cpu"] = {"horizons": S, "both_converged": int(both.sum()),
+                             "same_status": int((st_gpu == st_cpu).sum()),
+                             "max_dq": float(np.abs(wq(w_gpu[both]) - wq(w_cpu[both])).max()) if both.any() else None}
+        result["cpu_baseline"] = rec
     if rank == 0:
         print(json.dumps(result))
     if world > 1:

@@ -159,6 +159,10 @@ int mf_solve_batch_ws_dev(mf_problem *p, int batch, const double *q0, const doub
 #define MF_NKERNELS 5
 int mf_problem_timing(mf_problem *p, int enable);
 int mf_problem_kernel_stats(const mf_problem *p, double *ms_total, long *launches);
+/* Per-chunk trace of the last solve run with timing on (the host polls the running count every 4
+ * iterations): iteration at the chunk start, problems running at its start, GPU ms of its launches.
+ * Fills up to `cap` entries of the non-null arrays; returns the number of chunks. */
+int mf_problem_trace(const mf_problem *p, int *iter, int *running, double *ms, int cap);
 const char *mf_kernel_name(int slot);
 
 /* ---- generic stage-structured OCPs: dual-arm box (C3), thermal fatigue state (a8) ----

@@ -7,6 +7,7 @@
 // without a usable device every compute entry point fails with MF_ERR_DEVICE.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -20,8 +21,8 @@
 
 namespace mf {
 bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevFrame *F, const OcpConst &C,
-                  const IpmArrays &A, int batch, hipStream_t s, double *w, int *status, int *iters, double *kkt,
-                  double *obj);
+                  const IpmArrays &A, int batch, int nact, hipStream_t s, double *w, int *status, int *iters,
+                  double *kkt, double *obj);
 }
 
 using namespace mf;
@@ -453,6 +454,10 @@ struct mf_problem {
     IpmArrays A;
     ProbState *d_st = nullptr;
     int *d_active = nullptr;
+    int *d_list = nullptr;  // compacted running set (batch) + its count
+    // per-chunk trace of the last timed solve: (iteration, running count, GPU ms of the chunk)
+    std::vector<int> tr_iter, tr_run;
+    std::vector<double> tr_ms;
 };
 
 static void free_ws(mf_problem *p) {
@@ -460,8 +465,10 @@ static void free_ws(mf_problem *p) {
     p->bufs.clear();
     if (p->d_st) (void)hipFree(p->d_st);
     if (p->d_active) (void)hipFree(p->d_active);
+    if (p->d_list) (void)hipFree(p->d_list);
     p->d_st = nullptr;
     p->d_active = nullptr;
+    p->d_list = nullptr;
     p->cap = 0;
 }
 
@@ -558,8 +565,11 @@ static int ensure_ws(mf_problem *p, int batch) {
     }
     HIPCHK(hipMalloc(&p->d_st, sizeof(ProbState) * (size_t)batch));
     HIPCHK(hipMalloc(&p->d_active, sizeof(int)));
+    HIPCHK(hipMalloc(&p->d_list, sizeof(int) * ((size_t)batch + 1)));
     A.st = p->d_st;
     A.active = p->d_active;
+    A.list = p->d_list;
+    A.nrun = p->d_list + batch;
     A.tau_lo = p->d_tlo;
     A.tau_hi = p->d_thi;
     p->cap = batch;
@@ -592,7 +602,8 @@ static int solve_core(mf_problem *p, int batch, const double *d_q0, const double
     }
     HIPCHK(hipMemcpyAsync(A.active, &batch, sizeof(int), hipMemcpyHostToDevice, s));
     DevFrame *F = p->d_frame;
-    if (!ipm_dispatch(n, C.nf, C.nl, 0, p->model->d_model, F, C, A, batch, s, nullptr, nullptr, nullptr, nullptr, nullptr))
+    if (!ipm_dispatch(n, C.nf, C.nl, 0, p->model->d_model, F, C, A, batch, batch, s, nullptr, nullptr, nullptr, nullptr,
+                      nullptr))
         return fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
     HIPCHK(hipGetLastError());
     int active = batch;
@@ -602,28 +613,45 @@ static int solve_core(mf_problem *p, int batch, const double *d_q0, const double
         p->ev.assign(2 * NPH * chunk, nullptr);
         for (auto &e2 : p->ev) HIPCHK(hipEventCreate(&e2));
     }
+    if (p->timing) {
+        p->tr_iter.clear();
+        p->tr_run.clear();
+        p->tr_ms.clear();
+    }
     for (int it = 0; it <= C.max_iter && active > 0; it += chunk) {
+        const int run_before = active;
         for (int c = 0; c < chunk; c++)
             for (int ph = 0; ph < NPH; ph++) {
                 if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * NPH + ph) * 2], s));
-                ipm_dispatch(n, C.nf, C.nl, 10 + ph, p->model->d_model, F, C, A, batch, s, nullptr, nullptr, nullptr,
-                             nullptr, nullptr);
+                ipm_dispatch(n, C.nf, C.nl, 10 + ph, p->model->d_model, F, C, A, batch, active, s, nullptr, nullptr,
+                             nullptr, nullptr, nullptr);
                 if (p->timing) HIPCHK(hipEventRecord(p->ev[(c * NPH + ph) * 2 + 1], s));
             }
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if (p->timing)
+        if (p->timing) {
+            double chunk_ms = 0.0;
             for (int c = 0; c < chunk; c++)
                 for (int ph = 0; ph < NPH; ph++) {
                     float ms = 0;
                     HIPCHK(hipEventElapsedTime(&ms, p->ev[(c * NPH + ph) * 2], p->ev[(c * NPH + ph) * 2 + 1]));
                     p->t_ms[ph] += ms;
                     p->t_launch[ph]++;
+                    chunk_ms += ms;
                 }
-        if (o && o->verbose) fprintf(stderr, "[mf] after %d iterations: %d running\n", it + chunk, active);
+            p->tr_iter.push_back(it);
+            p->tr_run.push_back(run_before);
+            p->tr_ms.push_back(chunk_ms);
+        }
+        if (o && o->verbose) {
+            static thread_local std::chrono::steady_clock::time_point t_start;
+            if (it == 0) t_start = std::chrono::steady_clock::now();
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+            fprintf(stderr, "[mf] after %d iterations: %d running  t=%.2f ms\n", it + chunk, active, ms);
+        }
     }
-    ipm_dispatch(n, C.nf, C.nl, 2, p->model->d_model, F, C, A, batch, s, d_w, d_status, d_iters, d_kkt, d_obj);
+    ipm_dispatch(n, C.nf, C.nl, 2, p->model->d_model, F, C, A, batch, batch, s, d_w, d_status, d_iters, d_kkt, d_obj);
     HIPCHK(hipGetLastError());
     return MF_OK;
 }
@@ -791,6 +819,17 @@ extern "C" int mf_problem_timing(mf_problem *p, int enable) {
 extern "C" const char *mf_kernel_name(int slot) {
     static const char *names[MF_NKERNELS] = {"k_eval_node", "k_eval_asm", "k_ipm_pre", "k_ipm_kkt", "k_ipm_post"};
     return (slot >= 0 && slot < MF_NKERNELS) ? names[slot] : "";
+}
+
+extern "C" int mf_problem_trace(const mf_problem *p, int *iter, int *running, double *ms, int cap) {
+    if (!p) return fail(MF_ERR_ARG, "null problem");
+    const int n = (int)p->tr_iter.size();
+    for (int i = 0; i < n && i < cap; i++) {
+        if (iter) iter[i] = p->tr_iter[i];
+        if (running) running[i] = p->tr_run[i];
+        if (ms) ms[i] = p->tr_ms[i];
+    }
+    return n;
 }
 
 extern "C" int mf_problem_kernel_stats(const mf_problem *p, double *ms_total3, long *launches3) {

@@ -53,6 +53,9 @@ struct IpmArrays {
     // warm start in the w layout (batch x wsize)
     const double *qd0p, *w0;
     int *active;                    // device counter of running problems
+    // compacted running set (k_compact, once per iteration): list[0..*nrun) = running problems in
+    // index order; every per-iteration kernel maps its block / node slot through it
+    int *list, *nrun;
 };
 
 // sizes (doubles) per problem

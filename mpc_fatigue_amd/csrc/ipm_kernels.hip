@@ -188,6 +188,7 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     __shared__ DevFrame F;
     __shared__ double Ts[NPB][NJ], Cs[NPB][NJ];
     __shared__ double SCs[NPB][NJ][2];  // sin / cos of each node's joint angles
+    if ((long)blockIdx.x * NPB >= (long)*A.nrun * C.N) return;  // block past the running set (uniform)
     Ml.load(Mg);
     stage_lds(&F, Fg);
     constexpr int cls = CLS;  // direction class: 0 = q directions, 1 = qd directions (own launch)
@@ -195,11 +196,12 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     const int tid = threadIdx.x, wv = tid >> 6, ln = tid & 63;
     const int g = wv * (64 / NJ) + ln / NJ, j0 = ln % NJ, v = cls * NJ + j0;
     const int N = C.N;
+    const long nslots = (long)*A.nrun * N;  // nodes of the compacted running set
     const long node = (long)grp * NPB + g;
-    bool run = (ln < (64 / NJ) * NJ) && node < (long)batch * N;
+    bool run = (ln < (64 / NJ) * NJ) && node < nslots;
     int b = 0, k = 0;
     if (run) {
-        b = (int)(node / N);
+        b = A.list[node / N];
         k = (int)(node % N);
         run = A.st[b].status == ST_RUNNING;
     }
@@ -307,10 +309,11 @@ __global__ __launch_bounds__(256) void k_eval_asm(OcpConst C, IpmArrays A, int b
     const int tid = threadIdx.x, g = tid / NV, v = tid % NV;
     const int N = C.N;
     const long node = (long)blockIdx.x * NPB + g;
-    bool run = g < NPB && node < (long)batch * N;
+    if ((long)blockIdx.x * NPB >= (long)*A.nrun * N) return;  // block past the running set (uniform)
+    bool run = g < NPB && node < (long)*A.nrun * N;
     int b = 0, k = 0;
     if (run) {
-        b = (int)(node / N);
+        b = A.list[node / N];
         k = (int)(node % N);
         run = A.st[b].status == ST_RUNNING;
     }
@@ -490,8 +493,9 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
     __shared__ int perm[MB], piv[MB];
-    const int b = blockIdx.x, lane = threadIdx.x;
-    if (b >= batch) return;
+    const int lane = threadIdx.x;
+    if ((int)blockIdx.x >= *A.nrun) return;
+    const int b = A.list[blockIdx.x];
     ProbState st = A.st[b];
     if (st.status != ST_RUNNING) return;
     Ml.load(Mg);
@@ -783,8 +787,9 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
     __shared__ int perm[MB], piv[MB];
-    const int b = blockIdx.x, lane = threadIdx.x;
-    if (b >= batch) return;
+    const int lane = threadIdx.x;
+    if ((int)blockIdx.x >= *A.nrun) return;
+    const int b = A.list[blockIdx.x];
     ProbState st = A.st[b];
     if (st.status != ST_RUNNING) return;
     Ml.load(Mg);
@@ -1404,8 +1409,9 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
     __shared__ int perm[MB], piv[MB];
-    const int b = blockIdx.x, lane = threadIdx.x;
-    if (b >= batch) return;
+    const int lane = threadIdx.x;
+    if ((int)blockIdx.x >= *A.nrun) return;
+    const int b = A.list[blockIdx.x];
     ProbState st = A.st[b];
     if (st.status != ST_RUNNING) return;
     Ml.load(Mg);
@@ -1780,20 +1786,54 @@ __global__ __launch_bounds__(64) void k_ipm_output(OcpConst C, IpmArrays A, int 
     }
 }
 
+// ============================================================== running-set compaction
+// One block: list[0..nrun) = the problems still ST_RUNNING, in index order (wave ballots + a
+// 16-entry scan per 1024-problem chunk).  Run after k_ipm_init and after every k_ipm_post; the
+// per-iteration kernels then size their grids from the host's last count of running problems
+// (an upper bound of nrun, which only falls) and map slots through the list.
+__global__ __launch_bounds__(1024) void k_compact(IpmArrays A, int batch) {
+    __shared__ int wsum[16];
+    __shared__ int base;
+    const int tid = threadIdx.x, ln = tid & 63, wv = tid >> 6;
+    if (tid == 0) base = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < batch; c0 += 1024) {
+        const int b = c0 + tid;
+        const bool r = b < batch && A.st[b].status == ST_RUNNING;
+        const unsigned long long m = __ballot(r);
+        if (ln == 0) wsum[wv] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wv; w++) off += wsum[w];
+        if (r) A.list[off + __popcll(m & ((1ull << ln) - 1ull))] = b;
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int w = 0; w < 16; w++) t += wsum[w];
+            base += t;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) A.nrun[0] = base;
+}
+
 // ============================================================== host launchers
 template <int NJ, int NF, int NL>
 struct IpmLaunch {
     static void init(const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A, int batch,
                      hipStream_t s) {
         hipLaunchKernelGGL((k_ipm_init<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+        hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, A, batch);
     }
     // phase 0: node derivatives (k_eval_node), 1: stage-Hessian assembly (k_eval_asm),
     // 2..4: per-problem IPM phases (k_ipm_pre, k_ipm_kkt, k_ipm_post)
+    // grids cover `nact` problems (>= the running count), slots mapped through A.list
     static void iter(int phase, const DevModel *M, const DevFrame *F, const OcpConst &C, const IpmArrays &A,
-                     int batch, hipStream_t s) {
+                     int batch, int nact, hipStream_t s) {
         constexpr int NPB = 4 * (64 / NJ);        // k_eval_node: nodes per block (one direction class)
         constexpr int NPBA = 256 / (2 * NJ + NF);  // k_eval_asm: nodes per block
-        long nodes = (long)batch * C.N;
+        if (nact < 1) return;
+        long nodes = (long)nact * C.N;
         if (phase == 0) {
             const int nb = (int)((nodes + NPB - 1) / NPB);
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL, 0>), dim3(nb), dim3(256), 0, s, M, F, C, A, batch, nb);
@@ -1802,11 +1842,12 @@ struct IpmLaunch {
             hipLaunchKernelGGL((k_eval_asm<NJ, NF, NL>), dim3((unsigned)((nodes + NPBA - 1) / NPBA)), dim3(256), 0, s,
                                C, A, batch);
         } else if (phase == 2) {
-            hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
         } else if (phase == 3) {
-            hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
         } else {
-            hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(batch), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, A, batch);
         }
     }
     static void output(const OcpConst &C, const IpmArrays &A, int batch, double *w, int *status, int *iters,
@@ -1822,12 +1863,12 @@ using Ipm_6_1_2 = IpmLaunch<6, 1, 2>;
 using Ipm_6_0_0 = IpmLaunch<6, 0, 0>;
 
 bool ipm_dispatch(int n, int nf, int nl, int what, const DevModel *M, const DevFrame *F, const OcpConst &C,
-                  const IpmArrays &A, int batch, hipStream_t s, double *w, int *status, int *iters, double *kkt,
-                  double *obj) {
+                  const IpmArrays &A, int batch, int nact, hipStream_t s, double *w, int *status, int *iters,
+                  double *kkt, double *obj) {
 #define MF_CASE(NJ, NF, NL)                                                       \
     if (n == NJ && nf == NF && nl == NL) {                                        \
         if (what == 0) IpmLaunch<NJ, NF, NL>::init(M, F, C, A, batch, s);          \
-        else if (what >= 10 && what <= 14) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, s); \
+        else if (what >= 10 && what <= 14) IpmLaunch<NJ, NF, NL>::iter(what - 10, M, F, C, A, batch, nact, s); \
         else IpmLaunch<NJ, NF, NL>::output(C, A, batch, w, status, iters, kkt, obj, s); \
         return true;                                                              \
     }

@@ -145,6 +145,15 @@ class OCP:
                 out[name] = (float(ms[i]), int(n[i]))
         return out
 
+    def trace(self) -> dict:
+        """Per-chunk trace of the last timed solve (mf_problem_trace): iteration at the chunk start,
+        problems running at its start, GPU ms of the chunk's launches."""
+        L = _lib.lib()
+        n = _lib.check(L.mf_problem_trace(self._h, None, None, None, 0))
+        it, run, ms = np.zeros(n, np.int32), np.zeros(n, np.int32), np.zeros(n)
+        L.mf_problem_trace(self._h, _lib.iptr(it), _lib.iptr(run), _lib.dptr(ms), n)
+        return {"iter": it, "running": run, "ms": ms}
+
     def node_eval(self, x, u, line_ref=None):
         """(x, u) -> (xnext, g, cost, jac) for a batch of shooting nodes (mf_node_eval)."""
         n, nf, nl = self.n, self.nf, self.nl

@@ -53,7 +53,8 @@ class GOpts(C.Structure):
     _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
                 ("mu_init", C.c_double), ("init_zero", C.c_int), ("verbose", C.c_int), ("F_init", C.c_double),
                 ("w0", C.POINTER(C.c_double)), ("bound_relax", C.c_double),
-                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("dual_out", C.POINTER(C.c_double))]
+                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("dual_out", C.POINTER(C.c_double)),
+                ("node_cb", C.c_void_p), ("node_ctx", C.c_void_p), ("val_cb", C.c_void_p)]
 
 
 _lib = None
@@ -176,9 +177,9 @@ def w_size(g: GOCP) -> int:
 
 
 def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, verbose=0, F_init=0.0,
-         w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None):
+         w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None, node_cb=None, node_ctx=None, val_cb=None):
     o = GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), F_init, None, bound_relax, None,
-              max_soc, None)
+              max_soc, None, node_cb, node_ctx, val_cb)
     if dual_out is not None:
         o._d = dual_out
         o.dual_out = _p(dual_out)
@@ -202,7 +203,16 @@ def solve(spec: dict, **kw):
     return w, r
 
 
-def solve_batch(specs: list, nthreads: int = 0, **kw):
+def bind(L):
+    """Set the generic-solver argtypes on a library exporting mfg_* (the checker, or oracle/libmfcpu.so)."""
+    dp = C.POINTER(C.c_double)
+    L.mfg_solve.argtypes = [dp, dp, C.POINTER(GOCP), C.POINTER(GOpts), dp, C.POINTER(O.Result)]
+    L.mfg_solve_batch.argtypes = [dp, dp, C.POINTER(GOCP), C.c_int, C.POINTER(GOpts), dp, C.c_int,
+                                  C.POINTER(O.Result), C.c_int]
+    return L
+
+
+def solve_batch(specs: list, nthreads: int = 0, L=None, **kw):
     made = [make(s) for s in specs]
     arr = (GOCP * len(specs))()
     for i, (g, _) in enumerate(made):
@@ -212,7 +222,7 @@ def solve_batch(specs: list, nthreads: int = 0, **kw):
     ws = w_size(made[0][0])
     w = np.zeros((len(specs), ws))
     res = (O.Result * len(specs))()
-    err = lib().mfg_solve_batch(_p(b0), _p(b1), arr, len(specs), C.byref(op), _p(w), ws, res, nthreads)
+    err = (L or lib()).mfg_solve_batch(_p(b0), _p(b1), arr, len(specs), C.byref(op), _p(w), ws, res, nthreads)
     if err:
         raise RuntimeError(f"mfg_solve_batch error {err}")
     return w, list(res)

@@ -81,6 +81,15 @@ typedef struct {
     const double *u_init;           /* initial control (nu) for every node, or NULL (0 / F_init) */
     int max_soc;                    /* IPOPT max_soc (second-order corrections per iteration; 0 = off) */
     double *dual_out;               /* diagnostics: [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU | mu] or NULL */
+    /* optional node-record provider (CPU baseline: the product's forward-over-reverse node functions
+     * compiled for the host, oracle/cpu_fast.cpp); NULL = the hyper-dual restatement below.  Record layout
+     * [l | grad l | c_in | d c_in | c_eq | d c_eq/dx | f | A | B | W] as csrc/gfam.hpp. */
+    int (*node_cb)(void *ctx, const double *xu, const double *yi, const double *ye, const double *lam,
+                   const double *lref, int eqon, double *rec);
+    void *node_ctx;
+    /* optional value provider of the same library (l, c_in, c_eq, f at one node); NULL = hyper-dual */
+    int (*val_cb)(void *ctx, const double *x, const double *u, const double *lref, double *l, double *ci,
+                  double *ce, double *f);
 } mfg_opts;
 
 typedef struct {
@@ -171,6 +180,7 @@ static void node_hd(const mfg_ocp *P, const models_t *MM, const hd *xu, hd *l, h
 /* ------------------------------------------------------------------ workspace */
 typedef struct {
     const mfg_ocp *P;
+    const mfg_opts *O;
     const models_t *MM;
     int N, nx, nu, nv, ni, ne, mb;
     /* per-variable masks (after relaxation) */
@@ -209,6 +219,10 @@ static int vfree(const ws_t *S, int k, int a) {
 
 static void eval_values(const ws_t *S, int k, const double *x, const double *u, double *l, double *ci, double *ce,
                         double *f) {
+    if (S->O && S->O->val_cb) {
+        S->O->val_cb(S->O->node_ctx, x, u, S->P->line_ref, l, ci, ce, f);
+        return;
+    }
     hd xu[GV], hl, hci[GI], hce[GE], hf[GX];
     for (int a = 0; a < S->nx; a++) xu[a] = K(x[a]);
     for (int a = 0; a < S->nu; a++) xu[S->nx + a] = K(u[a]);
@@ -226,6 +240,35 @@ static void eval_derivs(ws_t *S, int k) {
     double *Af = S->Af + k * nx * nx, *Bf = S->Bf + k * nx * nu, *W = S->W + (size_t)k * nv * nv;
     const double *lam = S->lam + k * nx, *yi = S->yi + k * ni, *ye = S->ye + k * ne;
     const int eqon = EQ_ON(S, k);
+    if (S->O && S->O->node_cb) {
+        const int oGL = 1, oCI = oGL + nv, oJI = oCI + ni, oCE = oJI + ni * nv, oJE = oCE + ne, oF = oJE + ne * nx,
+                  oA = oF + nx, oB = oA + nx * nx, oW = oB + nx * nu, REC = oW + nv * nv;
+        double xu[GV], rec[2 * GV * GV + GV * GI + GX * GX + 512];
+        memcpy(xu, x, nx * sizeof(double));
+        memcpy(xu + nx, u, nu * sizeof(double));
+        S->O->node_cb(S->O->node_ctx, xu, yi, ye, lam, S->P->line_ref, eqon, rec);
+        (void)REC;
+        S->l[k] = rec[0];
+        memcpy(gl, rec + oGL, nv * sizeof(double));
+        memcpy(S->ci + k * ni, rec + oCI, ni * sizeof(double));
+        memcpy(Ji, rec + oJI, (size_t)ni * nv * sizeof(double));
+        memcpy(S->ce + k * ne, rec + oCE, ne * sizeof(double));
+        memcpy(Je, rec + oJE, (size_t)ne * nx * sizeof(double));
+        memcpy(S->f + k * nx, rec + oF, nx * sizeof(double));
+        memcpy(Af, rec + oA, (size_t)nx * nx * sizeof(double));
+        memcpy(Bf, rec + oB, (size_t)nx * nu * sizeof(double));
+        memcpy(W, rec + oW, (size_t)nv * nv * sizeof(double));
+        /* fixed variables carry no derivatives (their rows are identities in the KKT) */
+        for (int a = 0; a < nv; a++)
+            if (!vfree(S, k, a)) {
+                gl[a] = 0;
+                for (int r = 0; r < ni; r++) Ji[r * nv + a] = 0;
+                if (a < nx) { for (int e = 0; e < ne; e++) Je[e * nx + a] = 0; for (int j = 0; j < nx; j++) Af[j * nx + a] = 0; }
+                else for (int j = 0; j < nx; j++) Bf[j * nu + a - nx] = 0;
+                for (int b = 0; b < nv; b++) W[a * nv + b] = W[b * nv + a] = 0;
+            }
+        return;
+    }
     eval_values(S, k, x, u, S->l + k, S->ci + k * ni, S->ce + k * ne, S->f + k * nx);
     memset(gl, 0, sizeof(double) * nv);
     memset(Ji, 0, sizeof(double) * ni * nv);
@@ -675,7 +718,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     if (N < 1 || nx > GX || nu > GU || ni > GI || ne > GE || mb > BKMAX) return -2;
     ws_t SS, *S = &SS;
     memset(S, 0, sizeof *S);
-    S->P = P; S->MM = &MM;
+    S->P = P; S->O = O; S->MM = &MM;
     S->N = N; S->nx = nx; S->nu = nu; S->nv = nv; S->ni = ni; S->ne = ne; S->mb = mb;
     const double h_unused = P->h; (void)h_unused;
 

@@ -745,11 +745,13 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
             /* which component limits the primal fraction-to-boundary step? */
             double aq = 1, ad = 1, as_ = 1;
             for (int k = 1; k <= N; k++) for (int j = 0; j < n; j++) { int i = k * n + j;
-                if (has(QLO(j))) FTB_L(S->q[i], S->dq[i], QLO(j), aq); if (has(QHI(j))) FTB_U(S->q[i], S->dq[i], QHI(j), aq); }
+                if (has(QLO(j))) FTB_L(S->q[i], S->dq[i], QLO(j), aq);
+                if (has(QHI(j))) FTB_U(S->q[i], S->dq[i], QHI(j), aq); }
             int ks = -1, js = -1;
             for (int k = 0; k < N; k++) for (int j = 0; j < n; j++) { int i = k * n + j; double old = as_;
                 if (k > 0) { if (has(DLO(j))) FTB_L(S->qd[i], S->dqd[i], DLO(j), ad); if (has(DHI(j))) FTB_U(S->qd[i], S->dqd[i], DHI(j), ad); }
-                if (has(TLO(k, j))) FTB_L(S->s[i], S->ds[i], TLO(k, j), as_); if (has(THI(k, j))) FTB_U(S->s[i], S->ds[i], THI(k, j), as_);
+                if (has(TLO(k, j))) FTB_L(S->s[i], S->ds[i], TLO(k, j), as_);
+                if (has(THI(k, j))) FTB_U(S->s[i], S->ds[i], THI(k, j), as_);
                 if (as_ < old) { ks = k; js = j; } }
             fprintf(stderr, "   ftb: q %.2e qd %.2e s %.2e (k %d j %d s %.3f ds %.3f tau %.3f lo %.2f hi %.2f)\n", aq, ad, as_, ks, js,
                     ks >= 0 ? S->s[ks * n + js] : 0, ks >= 0 ? S->ds[ks * n + js] : 0, ks >= 0 ? S->tau[ks * n + js] : 0,

@@ -16,15 +16,18 @@ import numpy as np
 from .urdf_np import Model
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "libmforacle.so")
+# MF_ORACLE_LIB: load another build of the checker instead (the sanitizer build, tests/test_sanitizers.py)
+LIB = os.environ.get("MF_ORACLE_LIB") or os.path.join(HERE, "libmforacle.so")
 MJ = 16
 BLOB_HDR = 4
 BLOB_JSTRIDE = 33
 
 
 def build(force: bool = False) -> str:
-    srcs = [os.path.join(HERE, f) for f in ("mf_oracle.c", "mf_ocp.c", "hd_kin.h", "Makefile")]
-    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(f) for f in srcs):
+    srcs = [os.path.join(HERE, f) for f in ("mf_oracle.c", "mf_ocp.c", "hd_kin.h", "cpu_fast.cpp", "Makefile")]
+    libs = [LIB, os.path.join(HERE, "libmfcpu.so")]
+    if force or not all(os.path.exists(x) for x in libs) or \
+            min(os.path.getmtime(x) for x in libs) < max(os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
     return LIB
 
@@ -35,7 +38,8 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        build()
+        if not os.environ.get("MF_ORACLE_LIB"):
+            build()
         L = C.CDLL(LIB)
         dp = C.POINTER(C.c_double)
         L.mfo_id.argtypes = [dp, dp, dp, dp, dp]

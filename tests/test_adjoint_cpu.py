@@ -19,10 +19,12 @@ from oracle.urdf_np import load_urdf_file
 from tests.conftest import ROOT
 
 NATIVE = os.path.join(ROOT, "tests", "native")
-LIB = os.path.join(NATIVE, "libadjcheck.so")
+LIB = os.environ.get("MF_ADJCHECK_LIB") or os.path.join(NATIVE, "libadjcheck.so")  # sanitizer build: tests/test_sanitizers.py
 
 
 def _build():
+    if os.environ.get("MF_ADJCHECK_LIB"):
+        return
     src = [os.path.join(NATIVE, "adjcheck.cpp"), os.path.join(ROOT, "mpc_fatigue_amd", "csrc", "urdf.cpp")]
     deps = src + [os.path.join(ROOT, "mpc_fatigue_amd", "csrc", h) for h in ("adj.hpp", "dyn.hpp", "model.hpp")]
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):

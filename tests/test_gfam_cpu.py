@@ -15,31 +15,17 @@ import pytest
 
 from mpc_fatigue_amd import problems as PR
 from oracle import generic as G
+from oracle.cpu_fast import GParams, gparams
 from tests.conftest import ROOT
 
 NATIVE = os.path.join(ROOT, "tests", "native")
-LIB = os.path.join(NATIVE, "libfamcheck.so")
+LIB = os.environ.get("MF_FAMCHECK_LIB") or os.path.join(NATIVE, "libfamcheck.so")  # sanitizer build: tests/test_sanitizers.py
 CSRC = os.path.join(ROOT, "mpc_fatigue_amd", "csrc")
-GX = 32
-
-
-class GParams(C.Structure):
-    """Mirror of mf::GParams (csrc/gfam.hpp)."""
-    _fields_ = [("N", C.c_int), ("h", C.c_double), ("eq_from", C.c_int),
-                ("nf", C.c_int), ("use_line", C.c_int), ("thermal", C.c_int), ("fdir", C.c_double * 9),
-                ("wF", C.c_double), ("wqd", C.c_double), ("wtau", C.c_double), ("wT", C.c_double),
-                ("th_a", C.c_double), ("th_b", C.c_double), ("Ra", C.c_double), ("Rh", C.c_double),
-                ("ktau", C.c_double * 16),
-                ("box_mg", C.c_double), ("box_L", C.c_double), ("box_pdes", C.c_double * 3), ("w_box", C.c_double),
-                ("w_qdb", C.c_double),
-                ("x_lo", C.c_double * GX), ("x_hi", C.c_double * GX),
-                ("tol", C.c_double), ("constr_viol_tol", C.c_double), ("mu_init", C.c_double), ("F_init", C.c_double),
-                ("max_iter", C.c_int), ("max_soc", C.c_int), ("init_zero", C.c_int), ("has_u_init", C.c_int),
-                ("u_init", C.c_double * GX), ("force_from", C.c_int), ("tier1_from", C.c_int),
-                ("tier1_to", C.c_int)]
 
 
 def _build():
+    if os.environ.get("MF_FAMCHECK_LIB"):
+        return
     src = [os.path.join(NATIVE, "famcheck.cpp"), os.path.join(CSRC, "urdf.cpp")]
     deps = src + [os.path.join(CSRC, h) for h in ("gfam.hpp", "adj.hpp", "dyn.hpp", "model.hpp")]
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(d) for d in deps):
@@ -60,26 +46,6 @@ def fam():
 
 def _p(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
-
-
-def gparams(spec):
-    g = GParams()
-    g.N, g.h, g.eq_from = spec["N"], spec["h"], 2
-    if spec.get("family") == "box":
-        g.box_mg, g.box_L, g.w_box, g.w_qdb = spec["box_mg"], spec["box_L"], spec["w_box"], spec["w_qd"]
-        g.box_pdes[:] = list(spec["p_des"])
-    else:
-        g.nf, g.use_line, g.thermal = spec["nf"], int(spec["use_line"]), int(spec.get("thermal", False))
-        fd = np.zeros(9)
-        fd[:3 * spec["nf"]] = np.asarray(spec["fdir"], float).reshape(-1)
-        g.fdir[:] = list(fd)
-        g.wF, g.wqd, g.wtau = spec["wF"], spec["wqd"], spec["wtau"]
-        if g.thermal:
-            g.th_a, g.th_b, g.Ra, g.Rh = spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
-            kt = np.zeros(16)
-            kt[:6] = spec["ktau"]
-            g.ktau[:] = list(kt)
-    return g
 
 
 def compare(fam, family, spec, xu, nx, nu, ni, ne, seed=0):

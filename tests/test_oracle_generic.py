@@ -23,11 +23,11 @@ def q_traj(w, N, nx=12, nu=18):
     return np.array([w[:nx]] + [w[nx + k * (nu + nx) + nu: nx + (k + 1) * (nu + nx)] for k in range(N)])
 
 
-def box_homotopy(spec, max_soc=4):
+def box_homotopy(spec, max_soc=4, **kw):
     w, res = None, []
     for tol in PR.box_homotopy_tolerances():
         sp = dict(spec, pos_toll=tol)
-        w, r = G.solve(sp, w0=w, u_init=PR.box_u_init(spec), max_iter=1000, max_soc=max_soc)
+        w, r = G.solve(sp, w0=w, u_init=PR.box_u_init(spec), max_iter=1000, max_soc=max_soc, **kw)
         res.append(r)
     return w, res
 

@@ -2,7 +2,9 @@
 MI355X_MICROARCH.md HBM section), calibrated on the copy kernel of tools/traffic_run.py (known
 512 MiB read + 512 MiB written), written to profiles/pmc_traffic.json for bench.py.
 
-usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV [OUT_JSON [FP64_CSV]]
+usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV [OUT_JSON [FP64_CSV [NODES_JSON]]]
+NODES_JSON (written by tools/traffic_run.py) adds per-node-evaluation totals for k_eval_node, the
+unit bench.py scales by its own node-evaluation count (launch sizes vary with the running set).
 FP64_CSV (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 pass) adds executed FP64 flops per launch:
 64 lanes x (2 FMA + MUL + ADD) per wave instruction, an upper bound (masked lanes count).
 """
@@ -27,7 +29,7 @@ def load(fn, counter):
     return per
 
 
-def add_eval_phase(res):
+def add_eval_phase(res, node_evals=None):
     """k_eval_node as the solver's phase 0: the q-class and qd-class launches of one iteration
     (one each per iteration), summed -- the unit bench.py's HIP-event timing uses."""
     q, qd = res.get("k_eval_node[q]"), res.get("k_eval_node[qd]")
@@ -37,6 +39,14 @@ def add_eval_phase(res):
     for f in ("read_bytes_per_launch", "write_bytes_per_launch", "hbm_bytes_per_launch", "fp64_flops_per_launch"):
         if f in q and f in qd:
             ph[f] = q[f] + qd[f]
+    if node_evals:
+        ph["node_evals"] = node_evals
+        for f, g in (("hbm_bytes_per_launch", "hbm_bytes_per_node_eval"),
+                     ("read_bytes_per_launch", "read_bytes_per_node_eval"),
+                     ("write_bytes_per_launch", "write_bytes_per_node_eval"),
+                     ("fp64_flops_per_launch", "fp64_flops_per_node_eval")):
+            if f in ph:
+                ph[g] = ph[f] * ph["launches"] / node_evals
     res["k_eval_node"] = ph
 
 
@@ -69,7 +79,8 @@ def main():
                   "hbm_bytes_per_launch": rd + wt}
         if k in flops:
             res[k]["fp64_flops_per_launch"] = flops[k]
-    add_eval_phase(res)
+    nodes = json.load(open(sys.argv[5]))["node_evals"] if len(sys.argv) > 5 else None
+    add_eval_phase(res, nodes)
     json.dump(res, open(out_path, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

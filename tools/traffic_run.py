@@ -1,6 +1,8 @@
 """Program profiled by tools/pmc_traffic.sh: one calibration copy of a known byte count
 (elementwise torch copy, 512 MiB read + 512 MiB written) and one batched solve of the bench
-workload (C5, 8192 horizons by default).  usage: python tools/traffic_run.py [B]"""
+workload (C5, 8192 horizons by default).  usage: python tools/traffic_run.py [B [NODES_JSON]]
+NODES_JSON receives the solve's node-evaluation count (the per-node normaliser of the PMC totals)."""
+import json
 import os
 import sys
 
@@ -33,3 +35,5 @@ ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), B, ptrs, tol=1e-8, constr_viol_tol
 torch.cuda.synchronize()
 it = out["iters"].cpu()
 print("solve done: iterations mean", float(it.double().mean()), "node evaluations", int(((it + 1) * 100).sum()))
+if len(sys.argv) > 2:
+    json.dump({"node_evals": int(((it + 1) * 100).sum()), "batch": B}, open(sys.argv[2], "w"))
