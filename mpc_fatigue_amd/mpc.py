@@ -12,14 +12,22 @@ the previous solution (``python/Centauro_script/mpc_principal.py:357-377``,
 
 ``RecedingHorizon`` runs that loop for a batch of horizons through ``mf_solve_batch_ws``
 (the GPU init kernel pushes the warm start into the bounds exactly as the oracle does).
-The thermal restart ``T0 <- T_N - 0.05`` belongs to the thermal state (row a8) that the
-Pilz transcriptions do not carry.
+
+``GRecedingHorizon`` runs it for the generic problems (gocp.GOCP: thermal state, dual arm)
+with the whole restart of ``mpc_principal.py:365-374``:
+
+* ``T_0 <- T_N - 0.05`` for the winding temperatures,
+* every restart value rounded to 4 decimals (``np.round(., 4)``, L371-373),
+* the warm start and the next initial state kept on the device: the previous solution
+  vector is the next solve's ``w0`` (ping-pong buffers, mf_gsolve_batch_dev) and the next
+  (x_0, qd_0) are sliced from it without a host round trip.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .ocp import OCP
+from .gocp import GOCP
+from .ocp import OCP, SolveResult
 
 
 def split_w(w: np.ndarray, n: int, nf: int, N: int):
@@ -65,3 +73,79 @@ class RecedingHorizon:
             qd = qdl if self.carry_velocity else None
             w0 = r.w
         return out
+
+
+def _round(x, decimals: int):
+    """np.round(x, decimals) (round half to even on x * 10^decimals) for numpy or torch arrays."""
+    if decimals is None:
+        return x
+    if isinstance(x, np.ndarray):
+        return np.round(x, decimals)
+    return x.round(decimals=decimals)
+
+
+def restart_state(w, nx: int, nu: int, N: int, n: int, thermal: bool, T_drop: float = 0.05,
+                  carry_velocity: bool = True, decimals: int | None = 4):
+    """(x_0, u_0) of the next horizon from solutions w (batch, wsize), numpy or torch:
+    x_0 = x_N (temperatures - T_drop), u_0 = u_{N-1} (its fixed part, the joint velocities, is
+    what the next horizon holds; zero without carry_velocity), both rounded (mpc_principal.py:365-373)."""
+    off = nx + (N - 1) * (nu + nx)
+    xN = w[:, off + nu:off + nu + nx]
+    x0 = xN.clone() if hasattr(xN, "clone") else xN.copy()
+    if thermal:
+        x0[:, n:2 * n] = x0[:, n:2 * n] - T_drop
+    u0 = w[:, off:off + nu] * (1.0 if carry_velocity else 0.0)
+    return _round(x0, decimals), _round(u0, decimals)
+
+
+class GRecedingHorizon:
+    """Repeated solves of a generic problem (gocp.GOCP) for a batch of initial states, restarted
+    as mpc_principal.py:357-377 restarts the Centauro MPC."""
+
+    def __init__(self, spec: dict, carry_velocity: bool = True, T_drop: float = 0.05, decimals: int | None = 4,
+                 models=None, **opts):
+        self.spec = spec
+        self.g = GOCP(spec, models=models)
+        self.n = self.g.models[0].nq if spec.get("family") != "box" else 12
+        self.thermal = bool(spec.get("thermal", False))
+        self.carry_velocity = carry_velocity
+        self.T_drop = T_drop
+        self.decimals = decimals
+        self.opts = opts
+
+    def next_initial(self, w):
+        g = self.g
+        return restart_state(w, g.nx, g.nu, g.N, self.n, self.thermal, self.T_drop, self.carry_velocity,
+                             self.decimals)
+
+    def run(self, x0, steps: int, u0=None, line_ref=None, device: int = 0) -> list:
+        """Device-resident loop; returns the per-step SolveResults (host copies)."""
+        import torch
+
+        g = self.g
+        dev = torch.device("cuda", device)
+        x = torch.as_tensor(np.atleast_2d(np.asarray(x0, float)), dtype=torch.float64, device=dev).contiguous()
+        B = x.shape[0]
+        u = None if u0 is None else torch.as_tensor(np.broadcast_to(np.asarray(u0, float), (B, g.nu)).copy(),
+                                                      dtype=torch.float64, device=dev)
+        lr = None if line_ref is None else torch.as_tensor(np.asarray(line_ref, float).reshape(B, 2),
+                                                           dtype=torch.float64, device=dev).contiguous()
+        wbuf = [torch.empty((B, g.wsize), dtype=torch.float64, device=dev) for _ in range(2)]
+        out = {"status": torch.empty(B, dtype=torch.int32, device=dev),
+               "iters": torch.empty(B, dtype=torch.int32, device=dev),
+               "kkt": torch.empty(B, dtype=torch.float64, device=dev),
+               "obj": torch.empty(B, dtype=torch.float64, device=dev)}
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        res, prev = [], None
+        for s in range(steps):
+            w = wbuf[s % 2]
+            ptr = {k: v.data_ptr() for k, v in out.items()}
+            ptr["w"] = w.data_ptr()
+            g.solve_dev(x.data_ptr(), None if u is None else u.data_ptr(), None if prev is None else prev.data_ptr(),
+                        None if lr is None else lr.data_ptr(), B, ptr, stream=stream, **self.opts)
+            res.append(SolveResult(w.cpu().numpy(), out["status"].cpu().numpy(), out["iters"].cpu().numpy(),
+                                   out["kkt"].cpu().numpy(), out["obj"].cpu().numpy()))
+            x, u = self.next_initial(w)
+            x, u = x.contiguous(), u.contiguous()
+            prev = w
+        return res

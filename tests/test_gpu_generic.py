@@ -107,3 +107,47 @@ def test_thermal_gpu_matches_oracle():
     w_ref, r_ref = G.solve(spec, F_init=PR.BENCH_F_INIT, max_iter=300, max_soc=4)
     assert r.status[0] == 0 and r_ref.status == 0
     np.testing.assert_allclose(r.w[0], w_ref, atol=1e-6)
+
+
+def _oracle_receding(spec, x0, steps, decimals, **kw):
+    """The restart of mpc_principal.py:357-377 on the oracle: x_0 <- x_N (T - 0.05), qd_0 <- qd_{N-1},
+    rounded to `decimals`, warm start = the previous solution."""
+    n, N = len(spec["q0"]), spec["N"]
+    g, _ = G.make(spec)
+    nx, nu = g.nx, g.nu
+    x, u, prev, out = np.asarray(x0, float), np.zeros(nu), None, []
+    rnd = (lambda a: np.round(a, decimals)) if decimals is not None else (lambda a: a)
+    for _ in range(steps):
+        sp = dict(spec, q0=list(x[:n]), T0=list(x[n:]), qd0=list(u[:n]))
+        w, r = G.solve(sp, w0=prev, **kw)
+        out.append((w, r))
+        off = nx + (N - 1) * (nu + nx)
+        xN = w[off + nu:off + nu + nx].copy()
+        xN[n:] -= 0.05
+        x, u, prev = rnd(xN), rnd(w[off:off + nu]), w
+    return out
+
+
+@pytest.mark.parametrize("decimals,steps", [(None, 4), (4, 2)])
+def test_thermal_receding_horizon_matches_oracle(decimals, steps):
+    """Thermal receding horizon (rows a8 + a14): T_0 <- T_N - 0.05, qd_0 <- qd_{N-1} carried, the
+    device-resident warm start, GPU = oracle at every step.  With the reference's 4-decimal rounding
+    the restart can land q_0 on a joint limit (here joint 3 at -2.35) and the next horizon is then
+    infeasible for both solvers -- the same status on both."""
+    from mpc_fatigue_amd.mpc import GRecedingHorizon
+
+    spec = PR.with_thermal(PR.pilz3_working(N=20), T0=20.0)
+    kw = dict(max_iter=300, max_soc=4)
+    x0 = np.r_[spec["q0"], spec["T0"]]
+    ref = _oracle_receding(spec, x0, steps, decimals, **kw)
+    loop = GRecedingHorizon(spec, carry_velocity=True, decimals=decimals, **kw)
+    res = loop.run(x0[None], steps)
+    for s, (r, (w_or, r_or)) in enumerate(zip(res, ref)):
+        assert r.status[0] == r_or.status, (s, r.status[0], r_or.status)
+        if r_or.status == 0:
+            np.testing.assert_allclose(r.w[0], w_or, atol=1e-6, err_msg=f"step {s}")
+    if decimals is None:
+        assert all(r_or.status == 0 for _, r_or in ref)
+        # the temperatures carried across restarts drop by T_drop at each restart
+        w1 = res[1].w[0]
+        np.testing.assert_allclose(w1[3:6], np.asarray(ref[0][0][-6:-3]) - 0.05, atol=1e-9)

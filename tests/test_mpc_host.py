@@ -33,3 +33,24 @@ def test_oracle_warm_start_from_solution():
     w2, r2 = O.solve(ref, sp, w0=w1, **opts)
     assert r1.status == 0 and r2.status == 0
     np.testing.assert_allclose(w2, w1, atol=1e-6)
+
+
+def test_generic_restart_state_rules():
+    """restart_state: x_0 <- x_N with T - 0.05, qd_0 <- qd_{N-1}, 4-decimal rounding
+    (mpc_principal.py:365-373), numpy path (GRecedingHorizon.next_initial on the device)."""
+    from mpc_fatigue_amd.mpc import restart_state
+
+    n, nx, nu, N = 3, 6, 3, 3
+    w = np.random.default_rng(0).normal(size=(2, nx + N * (nu + nx)))
+    x0, u0 = restart_state(w, nx, nu, N, n, True)
+    off = nx + (N - 1) * (nu + nx)
+    xN = w[:, off + nu:off + nu + nx]
+    np.testing.assert_array_equal(x0[:, :3], np.round(xN[:, :3], 4))
+    np.testing.assert_array_equal(x0[:, 3:], np.round(xN[:, 3:] - 0.05, 4))
+    np.testing.assert_array_equal(u0, np.round(w[:, off:off + nu], 4))
+    x0, u0 = restart_state(w, nx, nu, N, n, True, carry_velocity=False, decimals=None)
+    np.testing.assert_array_equal(u0, 0.0 * w[:, off:off + nu])
+    np.testing.assert_array_equal(x0[:, 3:], xN[:, 3:] - 0.05)
+    import torch
+    xt, ut = restart_state(torch.from_numpy(w), nx, nu, N, n, True)
+    np.testing.assert_array_equal(xt.numpy(), restart_state(w, nx, nu, N, n, True)[0])
