@@ -165,7 +165,7 @@ int mf_problem_kernel_stats(const mf_problem *p, double *ms_total, long *launche
 int mf_problem_trace(const mf_problem *p, int *iter, int *running, double *ms, int cap);
 const char *mf_kernel_name(int slot);
 
-/* ---- generic stage-structured OCPs: dual-arm box (C3), thermal fatigue state (a8) ----
+/* ---- generic stage-structured OCPs: dual-arm box (C3), thermal fatigue state (a8), Centauro (C4) ----
  * Replaces the per-node transcription loops of python/2_pilz_6_DOF/Box_Pilz_6DOF.py:219-456 and of
  * the thermal MPC (python/Centauro_script/RepeatedMPCwithThermal.py:183-402, Tmodel_library.py:9-41)
  * plus their nlpsol('ipopt') solves.  One horizon is the NLP
@@ -179,9 +179,18 @@ const char *mf_kernel_name(int slot);
  *   MF_FAM_BOX    two 6-DOF arms (model 0 = first, model 1 = second URDF), x = [q_L, q_R],
  *                 u = [qd_L, qd_R, F_L, F_R];  c_in = [F_L + F_R - (0, 0, m g) as (z, x, y),
  *                 (E1 - E2) x (F_L - F_R), tau_L, tau_R];  c_eq = |E1 - E2|^2 - L;
- *                 l = w_box |(E1 + E2)/2 - p_des|^2 + w_qd |qd|^2;  f = q + h qd            */
+ *                 l = w_box |(E1 + E2)/2 - p_des|^2 + w_qd |qd|^2;  f = q + h qd
+ *   MF_FAM_CENTAURO  two 7-DOF arms (models 0 / 1, frames mass1_ee / mass2_ee),
+ *                 python/Centauro_script/RepeatedMPCwithThermal.py:154-402 (Const1): x = [q (14), T (14)],
+ *                 u = [qd (14), F_L, F_R];  c_in = tau = ID(q, qd, 0) + J_LA^T [F_L; 0] + J_RA^T [F_R; 0];
+ *                 c_eq = [R_L^T (p_R - p_L), skew(R_L R_R^T)] minus their values at x_0 (rounded to
+ *                 target_decimals when >= 0, mpc_principal.py:371-373), k >= eq_from;  mixed rows for
+ *                 every k: F_L + F_R - (0, 0, m g) as (z, x, y), (p_L - p_R) x (F_L - F_R);
+ *                 l = w_box |(p_L + p_R)/2 - box_pdes|^2 + w_qd |qd|^2 + wF (|F_L|^2 + |F_R|^2) + wT |T|^2;
+ *                 f = [q + h qd, th_a T + th_b (Ra (tau/ktau)^2 + qd^2/Rh)]                      */
 #define MF_FAM_CHAIN 0
 #define MF_FAM_BOX 1
+#define MF_FAM_CENTAURO 2
 #define MF_GX_MAX 32
 typedef struct mf_gproblem mf_gproblem;
 typedef struct {
@@ -202,6 +211,7 @@ typedef struct {
     double x_lo[MF_GX_MAX], x_hi[MF_GX_MAX];         /* states k >= 1, +-inf allowed */
     const double *u_lo, *u_hi;                       /* N x nu */
     const double *c_lo, *c_hi;                       /* N x ni */
+    int target_decimals;                             /* CENTAURO: rounding of the pose targets, -1: exact */
 } mf_gspec;
 
 typedef struct {

@@ -53,7 +53,7 @@ MF_GX_MAX = 32
 
 
 class GSpec(C.Structure):
-    """mf_gspec (include/mpcfatigue.h): generic stage-structured OCP (box C3, thermal a8)."""
+    """mf_gspec (include/mpcfatigue.h): generic stage-structured OCP (box C3, thermal a8, Centauro C4)."""
     _fields_ = [
         ("family", C.c_int), ("N", C.c_int), ("h", C.c_double), ("frame0", C.c_int), ("frame1", C.c_int),
         ("eq_from", C.c_int), ("nf", C.c_int), ("fdir", C.c_double * 9), ("use_line", C.c_int),
@@ -65,6 +65,7 @@ class GSpec(C.Structure):
         ("x_lo", C.c_double * MF_GX_MAX), ("x_hi", C.c_double * MF_GX_MAX),
         ("u_lo", C.POINTER(C.c_double)), ("u_hi", C.POINTER(C.c_double)),
         ("c_lo", C.POINTER(C.c_double)), ("c_hi", C.POINTER(C.c_double)),
+        ("target_decimals", C.c_int),
     ]
 
 

@@ -46,14 +46,14 @@ struct GArrays {
     double *tx, *tu, *ts;
     double *P, *Kinv, *Kfb, *pv, *kv;
     const double *u_lo, *u_hi, *c_lo, *c_hi;  // shared, N x NU / N x NI
-    double *x0, *lref;                        // per problem: NX, 2
+    double *x0, *lref;                        // per problem: NX, FAM::LREF (line reference / pose targets)
     const double *u0, *w0;                    // optional per-problem fixed u_0 values / warm start
     GState *st;
     int *active;
 };
 
 template <class D> struct GSz {
-    static constexpr int NX = D::NX, NU = D::NU, NI = D::NIA, NE = D::NEA, NK = D::NU + D::NEA;
+    static constexpr int NX = D::NX, NU = D::NU, NI = D::NIA, NE = D::NET, NK = D::NU + D::NET;
     size_t N;
     __host__ __device__ GSz(int n) : N(n) {}
     __host__ __device__ size_t x() const { return (N + 1) * NX; }
@@ -161,8 +161,8 @@ __global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevMode
     }
     const GSz<D> Z(N);
     const double *x = A.x + b * Z.x() + (size_t)k * D::NX, *u = A.u + b * Z.u() + (size_t)k * D::NU;
-    const double *yi = A.yi + b * Z.i() + (size_t)k * D::NIA, *ye = A.ye + b * Z.e() + (size_t)k * D::NEA;
-    const double *lam = A.lam + b * Z.l() + (size_t)k * D::NX, *lref = A.lref + 2 * b;
+    const double *yi = A.yi + b * Z.i() + (size_t)k * D::NIA, *ye = A.ye + b * Z.e() + (size_t)k * D::NET;
+    const double *lam = A.lam + b * Z.l() + (size_t)k * D::NX, *lref = A.lref + FAM::LREF * b;
     const bool eqon = D::NE > 0 && k >= P.eq_from && k < N;
     if (run && t < FAM::PRE) FAM::prepass(M, F, P, x, u, t, S[g]);
     __syncthreads();
@@ -181,7 +181,7 @@ template <class FAM>
 __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                               const DevFrame *F1, GParams P, GArrays A, int batch) {
     using D = typename FAM::D;
-    constexpr int NX = D::NX, NU = D::NU, NI = D::NI, NIA = D::NIA, NEA = D::NEA;
+    constexpr int NX = D::NX, NU = D::NU, NI = D::NI, NIA = D::NIA, NET = D::NET;
     GMODELS(FAM);
     const int b = blockIdx.x, lane = threadIdx.x;
     if (b >= batch) return;
@@ -189,6 +189,10 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
     const GSz<D> Z(N);
     double *x = A.x + b * Z.x(), *u = A.u + b * Z.u(), *s = A.s + b * Z.i();
     const double *x0 = A.x0 + (size_t)b * NX;
+    if (FAM::LREF > 2) {  // per-problem data of the family computed from x_0 (Centauro pose targets)
+        if (lane == 0) FAM::targets(M, F, P, x0, A.lref + FAM::LREF * b);
+        gsync();
+    }
     const int wst = NU + NX, wsz = NX + N * wst;
     const double *w0 = A.w0 ? A.w0 + (size_t)b * wsz : nullptr;
     for (int e = lane; e < (N + 1) * NX; e += 64) {
@@ -216,12 +220,12 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         A.zuU[b * Z.u() + e] = (!fixed && gb(hi)) ? 1.0 : 0.0;
     }
     for (int e = lane; e < N * NX; e += 64) A.lam[b * Z.l() + e] = 0.0;
-    for (int e = lane; e < N * NEA; e += 64) A.ye[b * Z.e() + e] = 0.0;
+    for (int e = lane; e < N * NET; e += 64) A.ye[b * Z.e() + e] = 0.0;
     for (int e = lane; e < N * NIA; e += 64) A.yi[b * Z.i() + e] = 0.0;
     gsync();
     for (int k = lane; k < N; k += 64) {
-        double l, ci[NIA], ce[NEA], f[NX];
-        FAM::values(M, F, P, x + (size_t)k * NX, u + (size_t)k * NU, A.lref + 2 * b, l, ci, ce, f);
+        double l, ci[NIA], ce[NET], f[NX];
+        FAM::values(M, F, P, x + (size_t)k * NX, u + (size_t)k * NU, A.lref + FAM::LREF * b, l, ci, ce, f);
         for (int r = 0; r < NI; r++) {
             const int i = k * NIA + r;
             const double lo = A.c_lo[k * NI + r], hi = A.c_hi[k * NI + r];
@@ -245,7 +249,8 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                                               const DevFrame *F1, GParams P, GArrays A, int batch) {
     using D = typename FAM::D;
     constexpr int NX = D::NX, NU = D::NU, NV = D::NV, NI = D::NI, NE = D::NE, NIA = D::NIA, NEA = D::NEA;
-    constexpr int NK = NU + NEA, LDK = NK + 1;
+    constexpr int NM = D::NM, NET = D::NET;  // mixed rows c_m(x_k, u_k): multipliers at ye[k NET + NEA + m]
+    constexpr int NK = NU + NET, LDK = NK + 1;
     const int b = blockIdx.x, lane = threadIdx.x;
     if (b >= batch) return;
     GState st = A.st[b];
@@ -279,7 +284,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     double *Pg = A.P + b * Z.P(), *Kg = A.Kinv + b * Z.Kinv(), *Fg = A.Kfb + b * Z.Kfb(), *pvg = A.pv + b * Z.l();
     double *kvg = A.kv + b * Z.kv();
     const double *ulo = A.u_lo, *uhi = A.u_hi, *clo = A.c_lo, *chi = A.c_hi;
-    const double *lref = A.lref + 2 * b;
+    const double *lref = A.lref + FAM::LREF * b;
     auto R = [&](int k) { return rec + (size_t)k * D::REC; };
     auto ufix = [&](int i) { return gb(ulo[i]) && ulo[i] == uhi[i]; };
     auto cact = [&](int k, int q) { return gb(clo[k * NI + q]) || gb(chi[k * NI + q]); };
@@ -321,7 +326,8 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             for (int jj = 0; jj < NX; jj++) r += rk[D::O_A + jj * NX + j] * lam[k * NX + jj];
             for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + j] * yi[k * NIA + q];
             if (eqon(k))
-                for (int ee = 0; ee < NE; ee++) r += rk[D::O_JE + ee * NX + j] * ye[k * NEA + ee];
+                for (int ee = 0; ee < NE; ee++) r += rk[D::O_JE + ee * NX + j] * ye[k * NET + ee];
+            for (int m = 0; m < NM; m++) r += rk[D::O_JM + m * NV + j] * ye[k * NET + NEA + m];
         }
         r += -zxL[i] + zxU[i];
         dinf = fmax(dinf, fabs(r));
@@ -335,6 +341,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         double r = rk[D::O_GL + NX + j];
         for (int jj = 0; jj < NX; jj++) r += rk[D::O_B + jj * NU + j] * lam[k * NX + jj];
         for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + NX + j] * yi[k * NIA + q];
+        for (int m = 0; m < NM; m++) r += rk[D::O_JM + m * NV + NX + j] * ye[k * NET + NEA + m];
         r += -zuL[e] + zuU[e];
         dinf = fmax(dinf, fabs(r));
         if (gb(ulo[e])) comp(zuL[e], u[e] - ulo[e]);
@@ -361,7 +368,14 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             const int k = e / NE, ee = e % NE;
             if (!eqon(k)) continue;
             pinf = fmax(pinf, fabs(R(k)[D::O_CE + ee]));
-            sm += fabs(ye[k * NEA + ee]);
+            sm += fabs(ye[k * NET + ee]);
+            nm++;
+        }
+    if (NM > 0)
+        for (int e = lane; e < N * NM; e += 64) {
+            const int k = e / NM, m = e % NM;
+            pinf = fmax(pinf, fabs(R(k)[D::O_CM + m]));
+            sm += fabs(ye[k * NET + NEA + m]);
             nm++;
         }
     dinf = wave_max(dinf); pinf = wave_max(pinf); cinf0 = wave_max(cinf0); cinfm = wave_max(cinfm);
@@ -429,9 +443,9 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         rin[i] = cact(k, q) ? R(k)[D::O_CI + q] - s[i] : 0.0;
     }
     for (int e = lane; e < N * NX; e += 64) rdyn[e] = R(e / NX)[D::O_F + e % NX] - x[(e / NX + 1) * NX + e % NX];
-    for (int e = lane; e < N * NEA; e += 64) {
-        const int k = e / NEA, ee = e % NEA;
-        req[e] = (ee < NE && eqon(k)) ? R(k)[D::O_CE + ee] : 0.0;
+    for (int e = lane; e < N * NET; e += 64) {
+        const int k = e / NET, ee = e % NET;
+        req[e] = ee < NEA ? ((ee < NE && eqon(k)) ? R(k)[D::O_CE + ee] : 0.0) : R(k)[D::O_CM + ee - NEA];
     }
     gsync();
 
@@ -498,10 +512,12 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                         for (int l = 0; l < NX; l++) v += Bb[l * NU + a] * T1[l * NU + c];
                     }
                 } else if (a >= NU && c >= NU) {
-                    v = (a == c) ? ((en && a - NU < NE) ? -dc : -1.0) : 0.0;
+                    v = (a == c) ? ((a - NU >= NEA || (en && a - NU < NE)) ? -dc : -1.0) : 0.0;
                 } else {
                     const int ee = (a >= NU ? a : c) - NU, uu = a >= NU ? c : a;
-                    if (en && ee < NE && !ufix(k * NU + uu))
+                    if (ufix(k * NU + uu)) v = 0.0;
+                    else if (ee >= NEA) v = rk[D::O_JM + (ee - NEA) * NV + NX + uu];  // mixed row of stage k
+                    else if (en && ee < NE)
                         for (int l = 0; l < NX; l++) v += Jn[ee * NX + l] * Bb[l * NU + uu];
                 }
                 Ks[a * LDK + c] = v;
@@ -515,6 +531,8 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                             v = Hs[(NX + a) * NV + j];
                             for (int l = 0; l < NX; l++) v += Bb[l * NU + a] * T2[l * NX + j];
                         }
+                    } else if (a - NU >= NEA) {
+                        v = rk[D::O_JM + (a - NU - NEA) * NV + j];
                     } else if (en && a - NU < NE) {
                         for (int l = 0; l < NX; l++) v += Jn[(a - NU) * NX + l] * Ab[l * NX + j];
                     }
@@ -530,7 +548,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             __syncthreads();
             const BKInertia in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
             if (in.zero) return 2;
-            if (in.pos != NU || in.neg != NEA) return 1;
+            if (in.pos != NU || in.neg != NET) return 1;
             // the stage factorisation is kept (the solves of the vector pass and of the second-order
             // corrections reuse it: a backward-stable LDL^T solve, not an explicit inverse)
             double *kst = Kg + (size_t)k * KSTG;
@@ -583,11 +601,12 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                         g += gx[k * NX + a] - (k > 0 ? lam[(k - 1) * NX + a] : 0.0);
                         for (int jj = 0; jj < NX; jj++) g += rk[D::O_A + jj * NX + a] * lam[k * NX + jj];
                         if (eqon(k))
-                            for (int ee = 0; ee < NE; ee++) g += rk[D::O_JE + ee * NX + a] * ye[k * NEA + ee];
+                            for (int ee = 0; ee < NE; ee++) g += rk[D::O_JE + ee * NX + a] * ye[k * NET + ee];
                     } else {
                         g += gu[k * NU + a - NX];
                         for (int jj = 0; jj < NX; jj++) g += rk[D::O_B + jj * NU + a - NX] * lam[k * NX + jj];
                     }
+                    for (int m = 0; m < NM; m++) g += rk[D::O_JM + m * NV + a] * ye[k * NET + NEA + m];
                 }
                 vx[a] = g;
             }
@@ -604,9 +623,11 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                         z = vx[NX + a];
                         for (int l = 0; l < NX; l++) z += rk[D::O_B + l * NU + a] * tv[l];
                     }
+                } else if (a - NU >= NEA) {
+                    z = re[k * NET + a - NU];  // mixed row of stage k
                 } else if (en && a - NU < NE) {
                     const int ee = a - NU;
-                    z = re[(k + 1) * NEA + ee];
+                    z = re[(k + 1) * NET + ee];
                     for (int l = 0; l < NX; l++) z += R(k + 1)[D::O_JE + ee * NX + l] * rd[k * NX + l];
                 }
                 zv[a] = z;
@@ -637,7 +658,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         }
         // forward sweep
         for (int j = lane; j < NX; j += 64) { dxs[j] = 0.0; dx[j] = 0.0; }
-        for (int ee = lane; ee < NEA; ee += 64) dye[ee] = 0.0;
+        for (int ee = lane; ee < NEA; ee += 64) dye[ee] = 0.0;  // state rows of node 0 (inactive)
         gsync();
         for (int k = 0; k < N; k++) {
             const double *rk = R(k);
@@ -666,7 +687,8 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                 dx[(k + 1) * NX + j] = dxn[j];
             }
             if (k + 1 < N)
-                for (int ee = lane; ee < NEA; ee += 64) dye[(k + 1) * NEA + ee] = (en && ee < NE) ? duv[NU + ee] : 0.0;
+                for (int ee = lane; ee < NEA; ee += 64) dye[(k + 1) * NET + ee] = (en && ee < NE) ? duv[NU + ee] : 0.0;
+            for (int m = lane; m < NM; m += 64) dye[k * NET + NEA + m] = duv[NU + NEA + m];
             gsync();
             for (int j = lane; j < NX; j += 64) dxs[j] = dxn[j];
             gsync();
@@ -750,12 +772,13 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         double fs = 0.0, t = 0.0, bar = 0.0;
         int bad = 0;
         for (int k = lane; k < N; k += 64) {
-            double l, ci[NIA], ce[NEA], f[NX];
+            double l, ci[NIA], ce[NET], f[NX];
             if (cur) {
                 const double *rk = R(k);
                 l = rk[D::O_L];
                 for (int q = 0; q < NI; q++) ci[q] = rk[D::O_CI + q];
                 for (int ee = 0; ee < NE; ee++) ce[ee] = rk[D::O_CE + ee];
+                for (int m = 0; m < NM; m++) ce[NE + m] = rk[D::O_CM + m];
                 for (int j = 0; j < NX; j++) f[j] = rk[D::O_F + j];
             } else {
                 FAM::values(M, F, P, xx + (size_t)k * NX, uu + (size_t)k * NU, lref, l, ci, ce, f);
@@ -775,7 +798,12 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             for (int ee = 0; ee < NEA; ee++) {
                 const double r = (eo && ee < NE) ? ce[ee] : 0.0;
                 t += fabs(r);
-                if (tre) tre[k * NEA + ee] = r;
+                if (tre) tre[k * NET + ee] = r;
+            }
+            for (int m = 0; m < NM; m++) {  // families write the mixed rows after their NE state rows
+                const double r = ce[NE + m];
+                t += fabs(r);
+                if (tre) tre[k * NET + NEA + m] = r;
             }
         }
         auto blog = [&](double v, double lo, double hi) {
@@ -817,7 +845,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     };
 
     // ---------------- inertia correction
-    double dw = 0.0, dc = 0.0, d1 = 0.0;
+    double dw = 0.0, dc = P.dc_always ? 1e-8 * pow(mu, 0.25) : 0.0, d1 = 0.0;
     int tier = st.reg_tier, step_no = 0;
     double reg = (st.reg_tier == 0) ? 0.0 : st.reg_last / 3.0;
     if (st.reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
@@ -893,7 +921,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             const double a_soc = alpha;
             for (int e = lane; e < N * NX; e += 64) sdyn[e] = alpha * rdyn[e] + trdyn[e];
             for (int e = lane; e < N * NIA; e += 64) sin_[e] = alpha * rin[e] + trin[e];
-            for (int e = lane; e < N * NEA; e += 64) seq[e] = alpha * req[e] + treq[e];
+            for (int e = lane; e < N * NET; e += 64) seq[e] = alpha * req[e] + treq[e];
             gsync();
             for (int p = 0; p < P.max_soc; p++) {
                 dir_copy(true);
@@ -917,7 +945,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                 th_old = ths;
                 for (int e = lane; e < N * NX; e += 64) sdyn[e] = aps * sdyn[e] + trdyn[e];
                 for (int e = lane; e < N * NIA; e += 64) sin_[e] = aps * sin_[e] + trin[e];
-                for (int e = lane; e < N * NEA; e += 64) seq[e] = aps * seq[e] + treq[e];
+                for (int e = lane; e < N * NET; e += 64) seq[e] = aps * seq[e] + treq[e];
                 gsync();
             }
             if (accepted) break;
@@ -935,7 +963,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     for (int e = lane; e < N * NU; e += 64) u[e] += alpha * du[e];
     for (int e = lane; e < N * NIA; e += 64) { s[e] += alpha * ds[e]; yi[e] += alpha * dyi[e]; }
     for (int e = lane; e < N * NX; e += 64) lam[e] += alpha * dlam[e];
-    for (int e = lane; e < N * NEA; e += 64) ye[e] += alpha * dye[e];
+    for (int e = lane; e < N * NET; e += 64) ye[e] += alpha * dye[e];
     gsync();
     auto zupd = [&](double &z, double dz, double sl) {
         const double zz = z + az * dz;
@@ -1023,12 +1051,13 @@ using namespace mf;
     } while (0)
 
 // the kernel instantiations (family, dims) and their dispatch
-enum GKind { GK_BOX = 0, GK_CH6F = 1, GK_CH6FT = 2, GK_CH3 = 3, GK_CH3T = 4 };
+enum GKind { GK_BOX = 0, GK_CH6F = 1, GK_CH6FT = 2, GK_CH3 = 3, GK_CH3T = 4, GK_CENT = 5 };
 using FamBox = BoxFam;
 using FamCh6F = ChainFam<6, 1, 2, false>;
 using FamCh6FT = ChainFam<6, 1, 2, true>;
 using FamCh3 = ChainFam<3, 0, 0, false>;
 using FamCh3T = ChainFam<3, 0, 0, true>;
+using FamCent = CentauroFam;
 
 struct mf_gproblem {
     mf_model *m0 = nullptr, *m1 = nullptr;
@@ -1059,7 +1088,7 @@ template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **
              {&A.trdyn, Z.l()}, {&A.trin, Z.i()}, {&A.treq, Z.e()}, {&A.sdyn, Z.l()}, {&A.sin_, Z.i()},
              {&A.seq, Z.e()},  {&A.tx, Z.x()},   {&A.tu, Z.u()},   {&A.ts, Z.i()},   {&A.P, Z.P()},
              {&A.Kinv, Z.Kinv()}, {&A.Kfb, Z.Kfb()}, {&A.pv, Z.l()}, {&A.kv, Z.kv()}, {&A.x0, (size_t)D::NX},
-             {&A.lref, 2}};
+             {&A.lref, (size_t)FAM::LREF}};
 }
 
 static void gfree_ws(mf_gproblem *p) {
@@ -1123,7 +1152,9 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     A.u0 = d_u0;
     A.w0 = d_w0;
     GHIPCHK(hipMemcpyAsync(A.x0, d_x0, sizeof(double) * D::NX * (size_t)batch, hipMemcpyDeviceToDevice, s));
-    if (d_lref) {
+    if (FAM::LREF != 2) {
+        // per-problem data computed by k_ginit from x_0
+    } else if (d_lref) {
         GHIPCHK(hipMemcpyAsync(A.lref, d_lref, sizeof(double) * 2 * (size_t)batch, hipMemcpyDeviceToDevice, s));
     } else {
         std::vector<double> lr(2 * (size_t)batch);
@@ -1165,6 +1196,7 @@ static int gdispatch_solve(mf_gproblem *p, int batch, const double *x0, const do
         case GK_CH6FT: return gsolve_core<FamCh6FT>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
         case GK_CH3: return gsolve_core<FamCh3>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
         case GK_CH3T: return gsolve_core<FamCh3T>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+        case GK_CENT: return gsolve_core<FamCent>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
     }
     return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }
@@ -1190,6 +1222,12 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
         if ((e = capi_model_dev(m1, &dM1, &h1))) return e;
         if (n0 != 6 || (int)h1->joints.size() != 6) return capi_fail(MF_ERR_UNSUPPORTED, "box family: two 6-joint arms");
         kind = GK_BOX;
+    } else if (spec->family == MF_FAM_CENTAURO) {
+        if (!m1) return capi_fail(MF_ERR_ARG, "the Centauro family needs two models");
+        if ((e = capi_model_dev(m1, &dM1, &h1))) return e;
+        if (n0 != 7 || (int)h1->joints.size() != 7)
+            return capi_fail(MF_ERR_UNSUPPORTED, "Centauro family: two 7-joint arms");
+        kind = GK_CENT;
     } else if (spec->family == MF_FAM_CHAIN) {
         const int ne = spec->use_line ? 2 : 0;
         if (n0 == 6 && spec->nf == 1 && ne == 2) kind = spec->thermal ? GK_CH6FT : GK_CH6F;
@@ -1218,6 +1256,7 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
         case GK_CH6FT: dims_of<FamCh6FT>(p->nx, p->nu, p->ni, p->ne); break;
         case GK_CH3: dims_of<FamCh3>(p->nx, p->nu, p->ni, p->ne); break;
         case GK_CH3T: dims_of<FamCh3T>(p->nx, p->nu, p->ni, p->ne); break;
+        case GK_CENT: dims_of<FamCent>(p->nx, p->nu, p->ni, p->ne); break;
     }
     const int N = spec->N;
     int rc = capi_frame_dev(m0, spec->frame0, &p->dF0);
@@ -1241,8 +1280,14 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
     P.w_box = spec->w_box; P.w_qdb = spec->w_qd;
     memcpy(P.x_lo, spec->x_lo, sizeof P.x_lo);
     memcpy(P.x_hi, spec->x_hi, sizeof P.x_hi);
+    P.target_decimals = spec->target_decimals;
     if (kind == GK_BOX) { P.force_from = 12; P.tier1_from = P.tier1_to = 0; }
-    else {
+    else if (kind == GK_CENT) {
+        // the moment rows at the fixed node 0 have rank 2 in F: IPOPT sees a singular KKT every
+        // iteration and perturbs it with delta_c; the solver does so from the first factorisation
+        P.force_from = 14; P.tier1_from = P.tier1_to = 0; P.dc_always = 1;
+        P.w_qdb = spec->w_qd;
+    } else {
         P.force_from = n0;
         const bool concave = spec->nf > 0 && spec->wF < 0;
         P.tier1_from = concave ? n0 : 0;
@@ -1343,11 +1388,14 @@ static int grec_core(mf_gproblem *p, const double *xu, const double *yi, const d
     using D = typename FAM::D;
     GBuf a, b2, c, d, l, o;
     int e;
-    if ((e = gh2d(a, xu, D::NV)) || (e = gh2d(b2, yi, D::NIA)) || (e = gh2d(l, lref, 2)) || (e = galloc(o, D::REC)))
+    if ((e = gh2d(a, xu, D::NV)) || (e = gh2d(b2, yi, D::NIA)) || (e = gh2d(l, lref, FAM::LREF)) ||
+        (e = galloc(o, D::REC)))
         return e;
-    std::vector<double> yev(D::NEA, 0.0);
+    // ye = [state rows (NE) | mixed rows (NM)] -> the device layout [NEA | NM]
+    std::vector<double> yev(D::NET, 0.0);
     for (int i = 0; i < D::NE; i++) yev[i] = ye[i];
-    if ((e = gh2d(c, yev.data(), D::NEA)) || (e = gh2d(d, lam, D::NX))) return e;
+    for (int i = 0; i < D::NM; i++) yev[D::NEA + i] = ye[D::NE + i];
+    if ((e = gh2d(c, yev.data(), D::NET)) || (e = gh2d(d, lam, D::NX))) return e;
     const DevModel *M1 = p->dM1 ? p->dM1 : p->dM0;
     const DevFrame *F1 = p->dF1 ? p->dF1 : p->dF0;
     hipLaunchKernelGGL(k_grec<FAM>, dim3(1), dim3(256), 0, 0, p->dM0, M1, p->dF0, F1, p->P, a.p, b2.p, c.p, d.p, l.p, o.p);
@@ -1384,6 +1432,7 @@ extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {
         case GK_CH6FT: return gdual_core<FamCh6FT>(p, b, out);
         case GK_CH3: return gdual_core<FamCh3>(p, b, out);
         case GK_CH3T: return gdual_core<FamCh3T>(p, b, out);
+        case GK_CENT: return gdual_core<FamCent>(p, b, out);
     }
     return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }
@@ -1394,9 +1443,9 @@ extern "C" int mf_gnode_record(mf_gproblem *p, const double *xu, const double *y
     int e = capi_ensure_device();
     if (e) return e;
     GHIPCHK(hipSetDevice(device));
-    const double zero2[2] = {p->spec.line_ref[0], p->spec.line_ref[1]};
-    const double *lr = line_ref ? line_ref : zero2;
-    const double ye0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const double zero2[6] = {p->spec.line_ref[0], p->spec.line_ref[1], 0, 0, 0, 0};
+    const double *lr = line_ref ? line_ref : zero2;  // CENTAURO: the 6 pose targets
+    const double ye0[16] = {0};
     const double *yv = ye ? ye : ye0;
     switch (p->kind) {
         case GK_BOX: return grec_core<FamBox>(p, xu, yi, yv, lam, lr, rec);
@@ -1404,6 +1453,7 @@ extern "C" int mf_gnode_record(mf_gproblem *p, const double *xu, const double *y
         case GK_CH6FT: return grec_core<FamCh6FT>(p, xu, yi, yv, lam, lr, rec);
         case GK_CH3: return grec_core<FamCh3>(p, xu, yi, yv, lam, lr, rec);
         case GK_CH3T: return grec_core<FamCh3T>(p, xu, yi, yv, lam, lr, rec);
+        case GK_CENT: return grec_core<FamCent>(p, xu, yi, yv, lam, lr, rec);
     }
     return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }

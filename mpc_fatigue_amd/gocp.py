@@ -1,4 +1,5 @@
-"""Generic stage-structured OCPs on the MI355X: the dual-arm box (C3) and thermal fatigue (a8).
+"""Generic stage-structured OCPs on the MI355X: the dual-arm box (C3), thermal fatigue (a8) and the
+Centauro thermal box lift (C4).
 
 Replaces the per-node transcription loops + ``nlpsol('ipopt')`` of
 ``python/2_pilz_6_DOF/Box_Pilz_6DOF.py:219-456`` and of the thermal MPC
@@ -23,7 +24,7 @@ from .ocp import SolveResult
 from .problems import box_homotopy_tolerances, box_u_init, read_urdf
 
 INF = float("inf")
-FAM_CHAIN, FAM_BOX = 0, 1
+FAM_CHAIN, FAM_BOX, FAM_CENTAURO = 0, 1, 2
 
 
 @dataclass
@@ -40,6 +41,14 @@ class GBounds:
 def bounds(spec: dict, n: int) -> GBounds:
     """Per-node bounds of a problem spec in the generic NLP form."""
     N = spec["N"]
+    if spec.get("family") == "centauro":
+        nq = 14
+        u_lo = np.hstack([np.tile(np.asarray(spec["qd_lo"], float), (N, 1)), np.full((N, 6), -INF)])
+        u_hi = np.hstack([np.tile(np.asarray(spec["qd_hi"], float), (N, 1)), np.full((N, 6), INF)])
+        u_lo[0, :nq] = u_hi[0, :nq] = np.asarray(spec["qd0"], float)
+        return GBounds(np.r_[spec["q_lo"], np.full(nq, spec["T_lo"])], np.r_[spec["q_hi"], np.full(nq, spec["T_hi"])],
+                       u_lo, u_hi, np.asarray(spec["tau_lo"], float), np.asarray(spec["tau_hi"], float),
+                       np.r_[spec["q0"], spec["T0"]])
     if spec.get("family") == "box":
         tol = spec["pos_toll"]
         c_lo = np.hstack([np.full((N, 6), -tol), np.asarray(spec["tau_lo"], float)])
@@ -73,13 +82,26 @@ class GOCP:
         urdfs = spec["urdf"] if isinstance(spec["urdf"], (list, tuple)) else [spec["urdf"]]
         self.models = models if models is not None else [_lib.Model(read_urdf(u)) for u in urdfs]
         n = self.models[0].nq
+        cent = spec.get("family") == "centauro"
         box = spec.get("family") == "box"
+        two = box or cent
         g = _lib.GSpec()
-        g.family = FAM_BOX if box else FAM_CHAIN
-        g.N, g.h, g.eq_from = spec["N"], spec["h"], 2
-        g.frame0 = self.models[0].frame_id(spec["frame"])
-        g.frame1 = self.models[1].frame_id(spec["frame"]) if box else 0
-        if box:
+        g.family = FAM_CENTAURO if cent else (FAM_BOX if box else FAM_CHAIN)
+        g.N, g.h, g.eq_from = spec["N"], spec["h"], (1 if cent else 2)
+        frames = spec.get("frames", [spec["frame"], spec["frame"]])
+        g.frame0 = self.models[0].frame_id(frames[0])
+        g.frame1 = self.models[1].frame_id(frames[1]) if two else 0
+        g.target_decimals = int(spec.get("target_decimals", -1))
+        self.nem = 6 if cent else 0
+        if cent:
+            g.box_mg, g.w_box, g.w_qd, g.wF = spec["box_mg"], spec["w_box"], spec["w_qd"], spec["wF"]
+            g.box_pdes[:] = list(spec["p_des"])
+            g.thermal, g.wT = 1, spec.get("wT", 0.0)
+            g.th_a, g.th_b, g.Ra, g.Rh = spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+            kt = np.zeros(_lib.MF_MAX_JOINTS)
+            kt[:14] = spec["ktau"]
+            g.ktau[:] = list(kt)
+        elif box:
             g.box_mg, g.box_L, g.w_box, g.w_qd = spec["box_mg"], spec["box_L"], spec["w_box"], spec["w_qd"]
             g.box_pdes[:] = list(spec["p_des"])
         else:
@@ -106,7 +128,7 @@ class GOCP:
         g.u_lo, g.u_hi, g.c_lo, g.c_hi = (_lib.dptr(a) for a in self._keep)
         self.bounds = bd
         h = C.c_void_p()
-        _lib.check(_lib.lib().mf_gproblem_create(self.models[0].handle, self.models[1].handle if box else None,
+        _lib.check(_lib.lib().mf_gproblem_create(self.models[0].handle, self.models[1].handle if two else None,
                                                  C.byref(g), C.byref(h)))
         self._h = h
         d = (C.c_int * 5)()
@@ -153,8 +175,10 @@ class GOCP:
                                                   stream))
 
     def node_record(self, xu, yi, ye, lam, line_ref=None, device: int = 0) -> np.ndarray:
-        """One node record from the device kernel (layout: mf_gnode_record)."""
-        arr = [np.ascontiguousarray(a, dtype=np.float64) for a in (xu, yi, ye if self.ne else np.zeros(1), lam)]
+        """One node record from the device kernel (layout: mf_gnode_record).  ye = [state rows | mixed rows];
+        line_ref: the line reference (chain) or the 6 pose targets (Centauro)."""
+        ne = self.ne + self.nem
+        arr = [np.ascontiguousarray(a, dtype=np.float64) for a in (xu, yi, ye if ne else np.zeros(1), lam)]
         lr = None if line_ref is None else np.ascontiguousarray(line_ref, dtype=np.float64)
         rec = np.zeros(8192)
         n = _lib.check(_lib.lib().mf_gnode_record(self._h, *[_lib.dptr(a) for a in arr],

@@ -103,10 +103,13 @@ class GRecedingHorizon:
     as mpc_principal.py:357-377 restarts the Centauro MPC."""
 
     def __init__(self, spec: dict, carry_velocity: bool = True, T_drop: float = 0.05, decimals: int | None = 4,
-                 models=None, **opts):
+                 models=None, restart_spec: dict | None = None, **opts):
+        """restart_spec: the problem solved from the second step on (the Centauro loop rounds its
+        relative-pose targets after the first solve, RepeatedMPCwithThermal.py:485-486); default spec."""
         self.spec = spec
         self.g = GOCP(spec, models=models)
-        self.n = self.g.models[0].nq if spec.get("family") != "box" else 12
+        self.g_restart = GOCP(restart_spec, models=self.g.models) if restart_spec is not None else self.g
+        self.n = len(spec["q0"])
         self.thermal = bool(spec.get("thermal", False))
         self.carry_velocity = carry_velocity
         self.T_drop = T_drop
@@ -141,8 +144,9 @@ class GRecedingHorizon:
             w = wbuf[s % 2]
             ptr = {k: v.data_ptr() for k, v in out.items()}
             ptr["w"] = w.data_ptr()
-            g.solve_dev(x.data_ptr(), None if u is None else u.data_ptr(), None if prev is None else prev.data_ptr(),
-                        None if lr is None else lr.data_ptr(), B, ptr, stream=stream, **self.opts)
+            (g if s == 0 else self.g_restart).solve_dev(
+                x.data_ptr(), None if u is None else u.data_ptr(), None if prev is None else prev.data_ptr(),
+                None if lr is None else lr.data_ptr(), B, ptr, stream=stream, **self.opts)
             res.append(SolveResult(w.cpu().numpy(), out["status"].cpu().numpy(), out["iters"].cpu().numpy(),
                                    out["kkt"].cpu().numpy(), out["obj"].cpu().numpy()))
             x, u = self.next_initial(w)

@@ -266,3 +266,61 @@ def pilz6_batch_q0(batch: int, seed: int = 0, spread: float = 0.05, q0=None) -> 
 def pilz6_bench(N: int = 100, q0=None, line_ref=(0.1, 0.4)) -> dict:
     """The benchmark instance of C2 (feasible fatigue floor, see BENCH_FLOOR)."""
     return pilz6_force(N=N, q0=q0, line_ref=line_ref, tau_floor=BENCH_FLOOR)
+
+
+# ---------------------------------------------------------------- C4: Centauro thermal box lift
+# Centauros_features.py:22-34 (limits of j_arm1_1..7, j_arm2_1..7)
+CENT_Q_LO = [-3.312, 0.020, -2.552, -2.465, -2.569, -1.529, -2.565, -3.3458, -3.4258, -2.5614, -2.4794, -2.5394,
+             -1.5154, -2.5554]
+CENT_Q_HI = [1.615, 3.431, 2.566, 0.280, 2.562, 1.509, 2.569, 1.6012, -0.0138, 2.5606, 0.2886, 2.5546, 1.5156, 2.5686]
+CENT_QD_LIM = [3.86, 3.86, 6.06, 6.06, 11.72, 11.72, 20.35] * 2
+CENT_TAU_LIM = [147.0, 147.0, 147.0, 147.0, 55.0, 55.0, 28.32] * 2
+_CQ0_FILE = os.path.join(HERE, "data", "centauro_q0.json")
+
+
+def centauro_q0() -> np.ndarray:
+    """IK start of the substitute arms (tools/centauro_ik.py: the problem of Centauro_functions.py:207-260)."""
+    with open(_CQ0_FILE) as f:
+        return np.array(json.load(f)["q0"], float)
+
+
+def centauro(N: int = 40, T: float = 30.0, q0=None, T0=20.0, qd0=None, mass: float = 10.0,
+             box_pos=(0.9, 0.0, 1.3), target_decimals: int = -1) -> dict:
+    """C4: the thermal Centauro MPC of ``python/Centauro_script/RepeatedMPCwithThermal.py`` (Const1:
+    full relative-pose constraints) on the substitute 7-DOF arms (tools/make_centauro_urdf.py; the
+    Centauro URDF is not in the reference).
+
+    x = [q(14), T(14)], u = [qd(14), F_L(3), F_R(3)] (L183-241, 376-391).  Per node k:
+    tau = ID(q, qd, 0) + J_LA^T [F_L; 0] + J_RA^T [F_R; 0] within +-joint_torque_lim (L341-350);
+    force / moment equilibrium = 0 for every k (mixed rows, L238-253); relative position
+    R_L^T (p_R - p_L) and orientation error of R_L R_R^T held at their x_0 values for k >= 1 (state
+    rows; the reference chains node k to node k-1, L255-272, and repeats the orientation rows,
+    L274-296 -- the same feasible set); T_{k+1} = a T_k + b (Ra (tau / ktau)^2 + qd^2 / Rh), T in
+    [0, 80] (L122-123, 365-402); cost 100 |p_box - box_pos|^2 + 100 qd^T qd + 10 |F_L|^2 + 10 |F_R|^2
+    (L353-356; the temperature term of L357-359 reads the numeric T_0, a constant).
+    target_decimals: round the relative-orientation target as the MPC restart does
+    (RepeatedMPCwithThermal.py:485-486); the relative-position rows keep x_0's exact value (they chain).
+    """
+    h = T / N
+    a, b = thermal_coeffs(h)
+    n = 14
+    tl = np.asarray(CENT_TAU_LIM, float)
+    return dict(
+        name="centauro", family="centauro",
+        urdf=["centauro_substitute_arm1.urdf", "centauro_substitute_arm2.urdf"], frames=["mass1_ee", "mass2_ee"],
+        frame="mass1_ee", N=N, h=h, n=n, nf=6, thermal=True,
+        q0=list(centauro_q0() if q0 is None else q0), qd0=list(np.zeros(n) if qd0 is None else qd0),
+        T0=list(np.broadcast_to(np.asarray(T0, float), (n,))), T_lo=0.0, T_hi=80.0,
+        q_lo=list(CENT_Q_LO), q_hi=list(CENT_Q_HI),
+        qd_lo=list(-np.asarray(CENT_QD_LIM)), qd_hi=list(CENT_QD_LIM),
+        tau_lo=np.tile(-tl, (N, 1)), tau_hi=np.tile(tl, (N, 1)),
+        th_a=a, th_b=b, Ra=TH_RA, Rh=TH_RH, ktau=list(KTAU14), wT=0.0,
+        box_mg=9.81 * mass, p_des=list(box_pos), w_box=100.0, w_qd=100.0, wF=10.0,
+        target_decimals=target_decimals,
+    )
+
+
+def centauro_u_init(spec: dict) -> np.ndarray:
+    """Initial controls of the first Centauro solve: qd = 0, each hand carrying half the box,
+    F = (0, 0, m g / 2) -- the reference's sol0 (RepeatedMPCwithThermal.py:148-151)."""
+    return np.r_[np.zeros(14), [0.0, 0.0, spec["box_mg"] / 2] * 2]

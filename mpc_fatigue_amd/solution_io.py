@@ -56,3 +56,31 @@ def unroll(w, spec: dict, model: _lib.Model | None = None) -> dict:
         Fw = F @ np.asarray(spec["fdir"], float).reshape(nf, 3)  # (N, 3) world force
         tau = tau - np.einsum("kri,kr->ki", J[:, :3, :], Fw)
     return {"q": q, "qd": qd, "F": F, "tau": tau}
+
+
+def centauro_split(w, N: int, thermal: bool = True, nq: int = 14) -> dict:
+    """Blocks of a Centauro solution vector.  Thermal layout (RepeatedMPCwithThermal.py:183-391):
+    [q_0, T_0 | (qd_k, F_L, F_R, q_{k+1}, T_{k+1}) x N]; non-thermal layout of the committed
+    Centauro_solutions/**/solution.csv (Centauro_dynamics.py / CentaurOCP.py):
+    [(q_k, qd_k, F_L, F_R) x N | q_N].  Returns q (N+1, nq), qd (N, nq), F (N, 6) and T (N+1, nq)."""
+    w = np.asarray(w, dtype=np.float64).ravel()
+    if thermal:
+        nx, nu = 2 * nq, nq + 6
+        blk = w[nx:].reshape(N, nu + nx)
+        x = np.vstack([w[:nx][None], blk[:, nu:]])
+        return {"q": x[:, :nq], "T": x[:, nq:], "qd": blk[:, :nq], "F": blk[:, nq:nu]}
+    st = 2 * nq + 6
+    blk = w[:N * st].reshape(N, st)
+    q = np.vstack([blk[:, :nq], w[N * st:][None]])
+    return {"q": q, "T": None, "qd": blk[:, nq:2 * nq], "F": blk[:, 2 * nq:st]}
+
+
+def centauro_invariants(w, N: int, h: float, mg: float, thermal: bool = True) -> dict:
+    """The checks a Centauro solution file must pass whatever the robot model:
+    explicit-Euler continuity max |q_{k+1} - q_k - h qd_k| and the force balance of the box,
+    max |F_Lz + F_Rz - m g| and max |F_L,xy + F_R,xy| (RepeatedMPCwithThermal.py:238-246)."""
+    b = centauro_split(w, N, thermal)
+    q, qd, F = b["q"], b["qd"], b["F"]
+    return {"continuity": float(np.abs(q[1:] - q[:-1] - h * qd).max()),
+            "force_z": float(np.abs(F[:, 2] + F[:, 5] - mg).max()),
+            "force_xy": float(np.abs(F[:, 0:2] + F[:, 3:5]).max())}

@@ -28,12 +28,16 @@ int record(const Ctx *c, const double *xu, const double *yi, const double *ye, c
     typename FAM::Scratch S;
     std::memset(&S, 0, sizeof S);
     const double *x = xu, *u = xu + D::NX;
-    const double ye0[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const double *yev = D::NE > 0 ? ye : ye0;
+    // the oracle passes ye = [state rows (NE) | mixed rows (NM)]; the families read [NEA | NM]
+    double yev[D::NET];
+    for (int i = 0; i < D::NET; i++) yev[i] = 0.0;
+    for (int i = 0; i < D::NE; i++) yev[i] = ye[i];
+    for (int i = 0; i < D::NM; i++) yev[D::NEA + i] = ye[D::NE + i];
+    const double *tg = lref;  // line reference (chain) or the 6 pose targets (Centauro)
     for (int t = 0; t < FAM::PRE; t++) FAM::prepass(c->M, c->F, c->P, x, u, t, S);
     FAM::seeds(c->P, u, yi, yev, lam, eqon != 0, S);
     for (int t = 0; t < FAM::LANES; t++) FAM::lane(c->M, c->F, x, u, yi, t, S);
-    for (int e = 0; e < D::REC; e++) rec[e] = FAM::rec(c->P, x, u, yi, yev, lam, eqon != 0, S, e, lref);
+    for (int e = 0; e < D::REC; e++) rec[e] = FAM::rec(c->P, x, u, yi, yev, lam, eqon != 0, S, e, tg);
     return D::REC;
 }
 
@@ -44,18 +48,19 @@ int frame_of(const Model &m, const char *name) {
 }
 }  // namespace
 
-// family: 0 box (urdf0 = first arm, urdf1 = second), 1 chain 6-DOF force + line, 2 the same with thermal state
-extern "C" void *mfc_create(int family, const char *urdf0, const char *urdf1, const char *frame, const GParams *P) {
+// family: 0 box, 1 chain 6-DOF force + line, 2 the same with thermal state, 3 Centauro (two 7-DOF arms)
+extern "C" void *mfc_create(int family, const char *urdf0, const char *urdf1, const char *frame0, const char *frame1,
+                            const GParams *P) {
     try {
         Ctx *c = new Ctx();
         c->family = family;
         Model m0 = build_model_from_urdf(urdf0);
         c->M[0] = make_dev_model(m0);
-        c->F[0] = make_dev_frame(m0, frame_of(m0, frame));
-        if (family == 0) {
+        c->F[0] = make_dev_frame(m0, frame_of(m0, frame0));
+        if (family == 0 || family == 3) {
             Model m1 = build_model_from_urdf(urdf1);
             c->M[1] = make_dev_model(m1);
-            c->F[1] = make_dev_frame(m1, frame_of(m1, frame));
+            c->F[1] = make_dev_frame(m1, frame_of(m1, frame1));
         } else {
             c->M[1] = c->M[0];
             c->F[1] = c->F[0];
@@ -76,6 +81,7 @@ extern "C" int mfc_node(void *ctx, const double *xu, const double *yi, const dou
         case 0: return record<BoxFam>(c, xu, yi, ye, lam, lref, eqon, rec);
         case 1: return record<ChainFam<6, 1, 2, false>>(c, xu, yi, ye, lam, lref, eqon, rec);
         case 2: return record<ChainFam<6, 1, 2, true>>(c, xu, yi, ye, lam, lref, eqon, rec);
+        case 3: return record<CentauroFam>(c, xu, yi, ye, lam, lref, eqon, rec);
     }
     return -5;
 }
@@ -83,8 +89,8 @@ extern "C" int mfc_node(void *ctx, const double *xu, const double *yi, const dou
 template <class FAM>
 int values(const Ctx *c, const double *x, const double *u, const double *lref, double *l, double *ci, double *ce,
            double *f) {
-    double ce0[8];
-    FAM::values(c->M, c->F, c->P, x, u, lref, *l, ci, FAM::D::NE > 0 ? ce : ce0, f);
+    double ce0[16];
+    FAM::values(c->M, c->F, c->P, x, u, lref, *l, ci, FAM::D::NE + FAM::D::NM > 0 ? ce : ce0, f);
     return 0;
 }
 
@@ -95,6 +101,7 @@ extern "C" int mfc_values(void *ctx, const double *x, const double *u, const dou
         case 0: return values<BoxFam>(c, x, u, lref, l, ci, ce, f);
         case 1: return values<ChainFam<6, 1, 2, false>>(c, x, u, lref, l, ci, ce, f);
         case 2: return values<ChainFam<6, 1, 2, true>>(c, x, u, lref, l, ci, ce, f);
+        case 3: return values<CentauroFam>(c, x, u, lref, l, ci, ce, f);
     }
     return -5;
 }

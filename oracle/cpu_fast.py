@@ -39,7 +39,7 @@ class GParams(C.Structure):
                 ("tol", C.c_double), ("constr_viol_tol", C.c_double), ("mu_init", C.c_double), ("F_init", C.c_double),
                 ("max_iter", C.c_int), ("max_soc", C.c_int), ("init_zero", C.c_int), ("has_u_init", C.c_int),
                 ("u_init", C.c_double * GX), ("force_from", C.c_int), ("tier1_from", C.c_int),
-                ("tier1_to", C.c_int)]
+                ("tier1_to", C.c_int), ("target_decimals", C.c_int), ("dc_always", C.c_int)]
 
 
 def gparams(spec: dict) -> GParams:
@@ -49,6 +49,15 @@ def gparams(spec: dict) -> GParams:
     if spec.get("family") == "box":
         g.box_mg, g.box_L, g.w_box, g.w_qdb = spec["box_mg"], spec["box_L"], spec["w_box"], spec["w_qd"]
         g.box_pdes[:] = list(spec["p_des"])
+    elif spec.get("family") == "centauro":
+        g.box_mg, g.w_box, g.w_qdb, g.wF = spec["box_mg"], spec["w_box"], spec["w_qd"], spec["wF"]
+        g.box_pdes[:] = list(spec["p_des"])
+        g.thermal, g.th_a, g.th_b, g.Ra, g.Rh = 1, spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+        g.wT = spec.get("wT", 0.0)
+        kt = np.zeros(16)
+        kt[:14] = spec["ktau"]
+        g.ktau[:] = list(kt)
+        g.target_decimals, g.dc_always, g.eq_from = int(spec.get("target_decimals", -1)), 1, 1
     else:
         g.nf, g.use_line, g.thermal = spec["nf"], int(spec["use_line"]), int(spec.get("thermal", False))
         fd = np.zeros(9)
@@ -72,7 +81,7 @@ def lib():
         O.build()
         L = C.CDLL(LIB)
         L.mfc_create.restype = C.c_void_p
-        L.mfc_create.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(GParams)]
+        L.mfc_create.argtypes = [C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(GParams)]
         L.mfc_free.argtypes = [C.c_void_p]
         assert L.mfc_gparams_size() == C.sizeof(GParams), "GParams mirror out of date"
         _lib = G.bind(L)
@@ -82,8 +91,10 @@ def lib():
 def family_code(spec: dict) -> int:
     if spec.get("family") == "box":
         return 0
+    if spec.get("family") == "centauro":
+        return 3
     if spec["nf"] != 1 or not spec["use_line"]:
-        raise ValueError("cpu_fast instantiates the box and the 6-DOF force+line chains only")
+        raise ValueError("cpu_fast instantiates the box, Centauro and the 6-DOF force+line chains only")
     return 2 if spec.get("thermal", False) else 1
 
 
@@ -97,8 +108,10 @@ class FastNodes:
         L = lib()
         names = spec["urdf"] if isinstance(spec["urdf"], (list, tuple)) else [spec["urdf"], spec["urdf"]]
         txt = [open(os.path.join(URDF_DIR, u), "rb").read() for u in names]
+        frames = spec.get("frames", [spec["frame"], spec["frame"]])
         self._g = gparams(spec)
-        self._ctx = L.mfc_create(family_code(spec), txt[0], txt[1], spec["frame"].encode(), C.byref(self._g))
+        self._ctx = L.mfc_create(family_code(spec), txt[0], txt[1], frames[0].encode(), frames[1].encode(),
+                                 C.byref(self._g))
         if not self._ctx:
             raise RuntimeError("mfc_create failed")
         self._L = L

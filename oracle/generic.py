@@ -19,7 +19,7 @@ from .urdf_np import load_urdf_file
 
 MJ = 16
 GX = 32
-MFG_CHAIN, MFG_BOX = 0, 1
+MFG_CHAIN, MFG_BOX, MFG_CENT = 0, 1, 2
 INF = float("inf")
 URDF_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpc_fatigue_amd", "urdf")
 
@@ -46,6 +46,8 @@ class GOCP(C.Structure):
         ("u_lo", C.POINTER(C.c_double)), ("u_hi", C.POINTER(C.c_double)),
         ("c_lo", C.POINTER(C.c_double)), ("c_hi", C.POINTER(C.c_double)),
         ("eq_from", C.c_int),
+        ("nem", C.c_int), ("relpos0", C.c_double * 3), ("orient0", C.c_double * 3), ("target_decimals", C.c_int),
+        ("dc_always", C.c_int),
     ]
 
 
@@ -96,7 +98,35 @@ def make(spec: dict):
     g.N, g.h = N, spec["h"]
     keep = []
     blobs = [O.model_blob(m) for m in ms]
-    if spec.get("family", "chain") == "box":
+    fam = spec.get("family", "chain")
+    g.target_decimals = -1
+    if fam == "centauro":
+        n = 14
+        g.family = MFG_CENT
+        g.nx, g.nu, g.ni, g.ne, g.nem = 2 * n, n + 6, n, 6, 6
+        g.force_from, g.tier1_from, g.tier1_to = n, 0, 0
+        for a, m in enumerate(ms):
+            g.frame[a][:] = list(O.frame_arr(m, spec["frames"][a]))
+        g.box_mg = spec["box_mg"]
+        g.box_pdes[:] = list(spec["p_des"])
+        g.w_box, g.w_qd, g.wF = spec["w_box"], spec["w_qd"], spec["wF"]
+        g.thermal = 1
+        g.th_a, g.th_b, g.Ra, g.Rh = spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+        kt = np.zeros(MJ)
+        kt[:n] = spec["ktau"]
+        g.ktau[:] = list(kt)
+        g.wT = spec.get("wT", 0.0)
+        g.target_decimals = int(spec.get("target_decimals", -1))
+        g.dc_always = 1
+        x_lo = np.r_[spec["q_lo"], np.full(n, spec["T_lo"])]
+        x_hi = np.r_[spec["q_hi"], np.full(n, spec["T_hi"])]
+        x0 = np.r_[spec["q0"], spec["T0"]]
+        c_lo, c_hi = np.asarray(spec["tau_lo"], float), np.asarray(spec["tau_hi"], float)
+        u_lo = np.hstack([np.tile(np.asarray(spec["qd_lo"], float), (N, 1)), np.full((N, 6), -INF)])
+        u_hi = np.hstack([np.tile(np.asarray(spec["qd_hi"], float), (N, 1)), np.full((N, 6), INF)])
+        u_lo[0, :n] = u_hi[0, :n] = np.asarray(spec["qd0"], float)
+        g.eq_from = 1
+    elif fam == "box":
         n = 12
         g.family = MFG_BOX
         g.nx, g.nu, g.ni, g.ne = n, n + 6, 6 + n, 1
@@ -233,8 +263,9 @@ def node_derivs(spec: dict, xu, yi, ye, lam):
     l + yi.c_in + ye.c_eq + lam.f."""
     g, (b0, b1) = make(spec)
     nv = g.nx + g.nu
-    no = 1 + g.ni + g.ne + g.nx
-    arrs = [np.ascontiguousarray(a, float) for a in (xu, yi, ye if g.ne else [0.0], lam)]
+    ne = g.ne + g.nem
+    no = 1 + g.ni + ne + g.nx
+    arrs = [np.ascontiguousarray(a, float) for a in (xu, yi, ye if ne else [0.0], lam)]
     vals, jac, H = np.zeros(no), np.zeros(no * nv), np.zeros(nv * nv)
     lib().mfg_node_derivs(_p(b0), _p(b1), C.byref(g), *[_p(a) for a in arrs], _p(vals), _p(jac), _p(H))
     return vals, jac.reshape(no, nv), H.reshape(nv, nv)

@@ -11,12 +11,15 @@
  *   min  sum_k l(x_k, u_k)
  *   s.t. x_{k+1} = f(x_k, u_k)                    explicit Euler (+ thermal recursion)
  *        c_lo[k] <= c_in(x_k, u_k) <= c_hi[k]     torques, equilibrium rows (slack rows)
- *        c_eq(x_k) = 0,  eq_from <= k < N         state-only equalities (line, distance)
+ *        c_eq(x_k) = 0,  eq_from <= k < N         state-only equalities (line, distance, relative pose)
+ *        c_m(x_k, u_k) = 0,  k < N                 mixed equalities (Centauro equilibrium rows)
  *        x_lo <= x_k <= x_hi (k >= 1), u_lo[k] <= u_k <= u_hi[k]  (lo == hi: fixed)
  * Families (node functions, hyper-dual so every derivative is exact):
  *   MFG_CHAIN  one serial arm: Pilz 3/6-DOF (C1, C2), optionally with the motor-winding
  *              thermal state T (Tmodel_library.py:9-41, RepeatedMPCwithThermal.py:371-376)
  *   MFG_BOX    two arms holding a box (C3, Box_Pilz_6DOF.py:219-456)
+ *   MFG_CENT   the Centauro thermal box lift (C4, RepeatedMPCwithThermal.py:154-402) on two 7-DOF
+ *              substitute arms: tau = ID + J^T W, relative pose, equilibrium, thermal state
  * Solver: the IPOPT-style primal-dual interior point of DESIGN.md section 4 (the same
  * iteration mf_oracle.c runs for the Pilz family), with a block-tridiagonal KKT over
  * shooting nodes factorised block by block with Bunch-Kaufman (inertia = sum over
@@ -36,10 +39,10 @@
 #define GU 32              /* max control size */
 #define GV (GX + GU)       /* max node variables */
 #define GI 48              /* max slack (inequality) rows */
-#define GE 8               /* max equality rows */
+#define GE 16              /* max equality rows (state + mixed) */
 #define GB (2 * GX + GU + GE)
 
-enum { MFG_CHAIN = 0, MFG_BOX = 1 };
+enum { MFG_CHAIN = 0, MFG_BOX = 1, MFG_CENT = 2 };
 
 typedef struct {
     int family;
@@ -67,6 +70,11 @@ typedef struct {
     const double *u_lo, *u_hi;      /* N x nu */
     const double *c_lo, *c_hi;      /* N x ni */
     int eq_from;
+    /* MFG_CENT (box_mg, box_pdes, w_box, w_qd, wF and the thermal fields above are shared) */
+    int nem;                        /* mixed equality rows c_m(x, u) after the ne state rows */
+    double relpos0[3], orient0[3];  /* relative-pose targets (set by the solver from x_0) */
+    int target_decimals;            /* round the targets (mpc_principal.py:371-373), -1: exact */
+    int dc_always;                  /* structurally rank-deficient equality rows: delta_c from the start */
 } mfg_ocp;
 
 typedef struct {
@@ -150,6 +158,68 @@ static void node_hd(const mfg_ocp *P, const models_t *MM, const hd *xu, hd *l, h
         *l = c;
         return;
     }
+    if (P->family == MFG_CENT) {
+        /* x = [q1(7) q2(7) T(14)], u = [qd(14) FL(3) FR(3)]  (RepeatedMPCwithThermal.py:183-402) */
+        const int na = MM->M[0].n, n2 = 2 * na;
+        const hd *T = xu + n2, *FL = u + n2, *FR = u + n2 + 3;
+        hd tau[2 * MJ], pL[3], pR[3], RL[9], RR[9], mF[3];
+        kin_t Kn;
+        hd zero[MJ];
+        for (int i = 0; i < na; i++) zero[i] = K(0);
+        /* tau_arm = ID(q, qd, 0) + J^T [F; 0]  (L341-345: the '+' sign; sub_external subtracts J^T Fw) */
+        for (int r = 0; r < 3; r++) mF[r] = muls(FL[r], -1.0);
+        kinematics(&MM->M[0], xu, &Kn);
+        rnea(&MM->M[0], &Kn, u, zero, tau);
+        frame_pose(&Kn, &MM->F[0], pL, RL);
+        sub_external(&MM->M[0], &Kn, &MM->F[0], pL, mF, tau);
+        for (int r = 0; r < 3; r++) mF[r] = muls(FR[r], -1.0);
+        kinematics(&MM->M[1], xu + na, &Kn);
+        rnea(&MM->M[1], &Kn, u + na, zero, tau + na);
+        frame_pose(&Kn, &MM->F[1], pR, RR);
+        sub_external(&MM->M[1], &Kn, &MM->F[1], pR, mF, tau + na);
+        for (int j = 0; j < n2; j++) ci[j] = tau[j];
+        /* state rows: relative position R_L^T (p_R - p_L) (L263-272) and orientation error of
+         * R_L R_R^T (L274-292, appended twice in the reference; once here) minus the targets */
+        hd d[3];
+        for (int r = 0; r < 3; r++) d[r] = sub(pR[r], pL[r]);
+        for (int b = 0; b < 3; b++)
+            ce[b] = sub(add(add(mul(RL[b], d[0]), mul(RL[3 + b], d[1])), mul(RL[6 + b], d[2])), K(P->relpos0[b]));
+        hd Ro[9];
+        for (int m = 0; m < 3; m++)
+            for (int nn = 0; nn < 3; nn++)
+                Ro[3 * m + nn] = add(add(mul(RL[3 * m], RR[3 * nn]), mul(RL[3 * m + 1], RR[3 * nn + 1])),
+                                     mul(RL[3 * m + 2], RR[3 * nn + 2]));
+        ce[3] = sub(muls(sub(Ro[7], Ro[5]), 0.5), K(P->orient0[0]));  /* ex = skew[2,1] */
+        ce[4] = sub(muls(sub(Ro[6], Ro[2]), 0.5), K(P->orient0[1]));  /* ey = skew[2,0] */
+        ce[5] = sub(muls(sub(Ro[3], Ro[1]), 0.5), K(P->orient0[2]));  /* ez = skew[1,0] */
+        /* mixed rows: force and moment equilibrium (L238-253) */
+        const int ne = P->ne;
+        ce[ne] = sub(add(FL[2], FR[2]), K(P->box_mg));
+        ce[ne + 1] = add(FL[0], FR[0]);
+        ce[ne + 2] = add(FL[1], FR[1]);
+        hd dd[3], dF[3], mom[3];
+        for (int r = 0; r < 3; r++) { dd[r] = sub(pL[r], pR[r]); dF[r] = sub(FL[r], FR[r]); }
+        cross3(mom, dd, dF);
+        for (int r = 0; r < 3; r++) ce[ne + 3 + r] = mom[r];
+        /* cost (L353-356): 100 |p_box - B|^2 + 100 qd^T qd + 10 |F_L|^2 + 10 |F_R|^2 (the thermal term of
+         * L357-359 is a constant: it reads the numeric T_0) */
+        hd c = K(0);
+        for (int r = 0; r < 3; r++) {
+            hd e = sub(muls(add(pL[r], pR[r]), 0.5), K(P->box_pdes[r]));
+            c = add(c, muls(mul(e, e), P->w_box));
+            c = add(c, muls(add(mul(FL[r], FL[r]), mul(FR[r], FR[r])), P->wF));
+        }
+        for (int j = 0; j < n2; j++) {
+            c = add(c, muls(mul(u[j], u[j]), P->w_qd));
+            f[j] = add(xu[j], muls(u[j], P->h));
+            hd ia = muls(tau[j], 1.0 / P->ktau[j]);
+            hd pl = add(muls(mul(ia, ia), P->Ra), muls(mul(u[j], u[j]), 1.0 / P->Rh));
+            f[n2 + j] = add(muls(T[j], P->th_a), muls(pl, P->th_b));
+            if (P->wT != 0.0) c = add(c, muls(mul(T[j], T[j]), P->wT));
+        }
+        *l = c;
+        return;
+    }
     /* MFG_BOX: x = [qL(6) qR(6)], u = [qdL(6) qdR(6) FL(3) FR(3)] */
     const int na = MM->M[0].n;
     const hd *qL = xu, *qR = xu + na, *qdL = u, *qdR = u + na, *FL = u + 2 * na, *FR = u + 2 * na + 3;
@@ -183,6 +253,7 @@ typedef struct {
     const mfg_opts *O;
     const models_t *MM;
     int N, nx, nu, nv, ni, ne, mb;
+    int nes;                         /* the first nes of the ne equality rows are state rows */
     /* per-variable masks (after relaxation) */
     double *ulo, *uhi, *clo, *chi;   /* N x nu, N x ni */
     double xlo[GX], xhi[GX];
@@ -207,9 +278,13 @@ typedef struct {
     double *bk;                      /* saved direction (second-order corrections) */
 } ws_t;
 
+/* per-problem data handed to the node callbacks: the line reference, or the Centauro pose targets
+ * (relpos0 and orient0 are adjacent: 6 values) */
+#define AUX(P) ((P)->family == MFG_CENT ? (P)->relpos0 : (P)->line_ref)
 static double *dal(size_t n) { return (double *)calloc(n ? n : 1, sizeof(double)); }
 
-#define EQ_ON(S, k) ((k) >= (S)->P->eq_from && (k) < (S)->N)
+/* equality row e of node k active: state rows for eq_from <= k < N, mixed rows for k < N */
+#define EQ_ON(S, k, e) ((k) < (S)->N && ((e) >= (S)->nes || (k) >= (S)->P->eq_from))
 #define CACT(S, k, r) (hasb((S)->clo[(k) * (S)->ni + (r)]) || hasb((S)->chi[(k) * (S)->ni + (r)]))
 /* free variable a (0..nv) of node k */
 static int vfree(const ws_t *S, int k, int a) {
@@ -220,7 +295,7 @@ static int vfree(const ws_t *S, int k, int a) {
 static void eval_values(const ws_t *S, int k, const double *x, const double *u, double *l, double *ci, double *ce,
                         double *f) {
     if (S->O && S->O->val_cb) {
-        S->O->val_cb(S->O->node_ctx, x, u, S->P->line_ref, l, ci, ce, f);
+        S->O->val_cb(S->O->node_ctx, x, u, AUX(S->P), l, ci, ce, f);
         return;
     }
     hd xu[GV], hl, hci[GI], hce[GE], hf[GX];
@@ -236,24 +311,29 @@ static void eval_values(const ws_t *S, int k, const double *x, const double *u, 
 static void eval_derivs(ws_t *S, int k) {
     const int nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne;
     const double *x = S->x + k * nx, *u = S->u + k * nu;
-    double *gl = S->gl + k * nv, *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + k * ne * nx;
+    double *gl = S->gl + k * nv, *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + (size_t)k * ne * nv;
     double *Af = S->Af + k * nx * nx, *Bf = S->Bf + k * nx * nu, *W = S->W + (size_t)k * nv * nv;
     const double *lam = S->lam + k * nx, *yi = S->yi + k * ni, *ye = S->ye + k * ne;
-    const int eqon = EQ_ON(S, k);
+    const int eqon = EQ_ON(S, k, 0), nes = S->nes, nem = ne - nes;
     if (S->O && S->O->node_cb) {
-        const int oGL = 1, oCI = oGL + nv, oJI = oCI + ni, oCE = oJI + ni * nv, oJE = oCE + ne, oF = oJE + ne * nx,
-                  oA = oF + nx, oB = oA + nx * nx, oW = oB + nx * nu, REC = oW + nv * nv;
+        /* record: ... | c_eq (nes) | d c_eq/dx (nes x nx) | c_m (nem) | d c_m (nem x nv) | f | A | B | W */
+        const int oGL = 1, oCI = oGL + nv, oJI = oCI + ni, oCE = oJI + ni * nv, oJE = oCE + nes, oCM = oJE + nes * nx,
+                  oJM = oCM + nem, oF = oJM + nem * nv, oA = oF + nx, oB = oA + nx * nx, oW = oB + nx * nu,
+                  REC = oW + nv * nv;
         double xu[GV], rec[2 * GV * GV + GV * GI + GX * GX + 512];
         memcpy(xu, x, nx * sizeof(double));
         memcpy(xu + nx, u, nu * sizeof(double));
-        S->O->node_cb(S->O->node_ctx, xu, yi, ye, lam, S->P->line_ref, eqon, rec);
+        S->O->node_cb(S->O->node_ctx, xu, yi, ye, lam, AUX(S->P), eqon, rec);
         (void)REC;
         S->l[k] = rec[0];
         memcpy(gl, rec + oGL, nv * sizeof(double));
         memcpy(S->ci + k * ni, rec + oCI, ni * sizeof(double));
         memcpy(Ji, rec + oJI, (size_t)ni * nv * sizeof(double));
-        memcpy(S->ce + k * ne, rec + oCE, ne * sizeof(double));
-        memcpy(Je, rec + oJE, (size_t)ne * nx * sizeof(double));
+        memcpy(S->ce + k * ne, rec + oCE, nes * sizeof(double));
+        memcpy(S->ce + k * ne + nes, rec + oCM, nem * sizeof(double));
+        memset(Je, 0, (size_t)ne * nv * sizeof(double));
+        for (int e = 0; e < nes; e++) memcpy(Je + e * nv, rec + oJE + e * nx, nx * sizeof(double));
+        memcpy(Je + nes * nv, rec + oJM, (size_t)nem * nv * sizeof(double));
         memcpy(S->f + k * nx, rec + oF, nx * sizeof(double));
         memcpy(Af, rec + oA, (size_t)nx * nx * sizeof(double));
         memcpy(Bf, rec + oB, (size_t)nx * nu * sizeof(double));
@@ -263,7 +343,8 @@ static void eval_derivs(ws_t *S, int k) {
             if (!vfree(S, k, a)) {
                 gl[a] = 0;
                 for (int r = 0; r < ni; r++) Ji[r * nv + a] = 0;
-                if (a < nx) { for (int e = 0; e < ne; e++) Je[e * nx + a] = 0; for (int j = 0; j < nx; j++) Af[j * nx + a] = 0; }
+                for (int e = 0; e < ne; e++) Je[e * nv + a] = 0;
+                if (a < nx) { for (int j = 0; j < nx; j++) Af[j * nx + a] = 0; }
                 else for (int j = 0; j < nx; j++) Bf[j * nu + a - nx] = 0;
                 for (int b = 0; b < nv; b++) W[a * nv + b] = W[b * nv + a] = 0;
             }
@@ -272,7 +353,7 @@ static void eval_derivs(ws_t *S, int k) {
     eval_values(S, k, x, u, S->l + k, S->ci + k * ni, S->ce + k * ne, S->f + k * nx);
     memset(gl, 0, sizeof(double) * nv);
     memset(Ji, 0, sizeof(double) * ni * nv);
-    memset(Je, 0, sizeof(double) * ne * nx);
+    memset(Je, 0, sizeof(double) * ne * nv);
     memset(Af, 0, sizeof(double) * nx * nx);
     memset(Bf, 0, sizeof(double) * nx * nu);
     memset(W, 0, sizeof(double) * nv * nv);
@@ -292,15 +373,15 @@ static void eval_derivs(ws_t *S, int k) {
             node_hd(S->P, S->MM, hx, &hl, hci, hce, hf);
             double h2 = hl.d;
             for (int r = 0; r < ni; r++) h2 += yi[r] * hci[r].d;
-            if (eqon)
-                for (int e = 0; e < ne; e++) h2 += ye[e] * hce[e].d;
+            for (int e = 0; e < ne; e++)
+                if (EQ_ON(S, k, e)) h2 += ye[e] * hce[e].d;
             for (int j = 0; j < nx; j++) h2 += lam[j] * hf[j].d;
             W[a * nv + b] = W[b * nv + a] = h2;
             if (a == b) {
                 gl[a] = hl.b;
                 for (int r = 0; r < ni; r++) Ji[r * nv + a] = hci[r].b;
+                for (int e = 0; e < ne; e++) Je[e * nv + a] = hce[e].b;
                 if (a < nx) {
-                    for (int e = 0; e < ne; e++) Je[e * nx + a] = hce[e].b;
                     for (int j = 0; j < nx; j++) Af[j * nx + a] = hf[j].b;
                 } else {
                     for (int j = 0; j < nx; j++) Bf[j * nu + a - nx] = hf[j].b;
@@ -348,9 +429,8 @@ static void merit_parts(const ws_t *S, const double *x, const double *u, const d
             th += fabs(r);
             if (rin) rin[k * ni + q] = r;
         }
-        const int eqon = EQ_ON(S, k);
         for (int e = 0; e < ne; e++) {
-            const double r = eqon ? ce[e] : 0.0;
+            const double r = EQ_ON(S, k, e) ? ce[e] : 0.0;
             th += fabs(r);
             if (req) req[k * ne + e] = r;
         }
@@ -378,7 +458,7 @@ static void residuals_cached(const ws_t *S, double *rdyn, double *rin, double *r
     for (int k = 0; k < N; k++) {
         for (int j = 0; j < nx; j++) rdyn[k * nx + j] = S->f[k * nx + j] - S->x[(k + 1) * nx + j];
         for (int q = 0; q < ni; q++) rin[k * ni + q] = CACT(S, k, q) ? S->ci[k * ni + q] - S->s[k * ni + q] : 0.0;
-        for (int e = 0; e < ne; e++) req[k * ne + e] = EQ_ON(S, k) ? S->ce[k * ne + e] : 0.0;
+        for (int e = 0; e < ne; e++) req[k * ne + e] = EQ_ON(S, k, e) ? S->ce[k * ne + e] : 0.0;
     }
 }
 
@@ -407,7 +487,7 @@ static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
         }
         if (k < N) {
             const double *W = S->W + (size_t)k * nv * nv, *Ji = S->Ji + (size_t)k * ni * nv;
-            const double *Je = S->Je + k * ne * nx;
+            const double *Je = S->Je + (size_t)k * ne * nv;
             double Dd[GI];
             for (int q = 0; q < ni; q++) {
                 const double sg = S->Ss[k * ni + q] + dw;
@@ -428,10 +508,9 @@ static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
                 }
                 D_(ox + a, ox + a) += dd;
             }
-            const int eqon = EQ_ON(S, k);
             for (int e = 0; e < ne; e++) {
-                if (eqon) {
-                    for (int j = 0; j < nx; j++) D_(oe + e, ox + j) = D_(ox + j, oe + e) = Je[e * nx + j];
+                if (EQ_ON(S, k, e)) {
+                    for (int j = 0; j < nv; j++) D_(oe + e, ox + j) = D_(ox + j, oe + e) = Je[e * nv + j];
                     D_(oe + e, oe + e) = -dc;
                 } else {
                     D_(oe + e, oe + e) = -1.0;
@@ -495,7 +574,7 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
         if (k > 0)
             for (int j = 0; j < nx; j++) r[ol + j] = -rdyn[(k - 1) * nx + j];
         if (k < N) {
-            const double *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + k * ne * nx;
+            const double *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + (size_t)k * ne * nv;
             double Dd[GI], rdd[GI];
             for (int q = 0; q < ni; q++) {
                 const int i = k * ni + q;
@@ -505,8 +584,7 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
                     rdd[q] = rin[i] + (S->gs[i] - S->yi[i]) / sg;
                 } else { Dd[q] = 0; rdd[q] = 0; }
             }
-            const int eqon = EQ_ON(S, k);
-            for (int e = 0; e < ne; e++) r[oe + e] = eqon ? -req[k * ne + e] : 0.0;
+            for (int e = 0; e < ne; e++) r[oe + e] = EQ_ON(S, k, e) ? -req[k * ne + e] : 0.0;
             for (int a = 0; a < nv; a++) {
                 if (!vfree(S, k, a)) { r[ox + a] = 0; continue; }
                 double g = S->gl[k * nv + a];
@@ -514,12 +592,12 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
                 if (a < nx) {
                     g += S->gx[k * nx + a] - (k > 0 ? S->lam[(k - 1) * nx + a] : 0.0);
                     for (int jj = 0; jj < nx; jj++) g += S->Af[(k * nx + jj) * nx + a] * S->lam[k * nx + jj];
-                    if (eqon)
-                        for (int e = 0; e < ne; e++) g += Je[e * nx + a] * S->ye[k * ne + e];
                 } else {
                     g += S->gu[k * nu + a - nx];
                     for (int jj = 0; jj < nx; jj++) g += S->Bf[(k * nx + jj) * nu + a - nx] * S->lam[k * nx + jj];
                 }
+                for (int e = 0; e < ne; e++)
+                    if (EQ_ON(S, k, e)) g += Je[e * nv + a] * S->ye[k * ne + e];
                 r[ox + a] = -g;
             }
         } else {
@@ -557,7 +635,7 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
                 if (k > 0) S->dlam[(k - 1) * nx + j] = y[ol + j];
             }
             for (int j = 0; j < nu; j++) S->du[k * nu + j] = S->ufix[k * nu + j] ? 0.0 : y[ou + j];
-            for (int e = 0; e < ne; e++) S->dye[k * ne + e] = EQ_ON(S, k) ? y[oe + e] : 0.0;
+            for (int e = 0; e < ne; e++) S->dye[k * ne + e] = EQ_ON(S, k, e) ? y[oe + e] : 0.0;
             memcpy(ynext, y, sizeof(double) * mb);
         }
     }
@@ -703,23 +781,41 @@ static void restore_direction(ws_t *S) {
     for (int i = 0; i < na; i++) { memcpy(*arr[i], S->bk + off, len[i] * sizeof(double)); off += len[i]; }
 }
 
+/* relative-pose targets of the Centauro rows from x_0: RelativePosition / RelativeOrientationError at
+ * q_0 (Centauro_functions.py:297-343).  The orientation target is optionally rounded as the MPC restart
+ * rounds RelativeOrientation_0 (RepeatedMPCwithThermal.py:485-486, np.round: half to even); the position
+ * rows chain node k to node k-1 in the reference (L255-272), so for k >= 1 they hold the exact value. */
+static void cent_targets(mfg_ocp *P, const models_t *MM) {
+    hd xu[GV], hl, hci[GI], hce[GE], hf[GX];
+    for (int i = 0; i < P->nx + P->nu; i++) xu[i] = K(i < P->nx ? P->x0[i] : 0.0);
+    for (int b = 0; b < 3; b++) P->relpos0[b] = P->orient0[b] = 0.0;
+    node_hd(P, MM, xu, &hl, hci, hce, hf);
+    const double sc = P->target_decimals >= 0 ? pow(10.0, P->target_decimals) : 0.0;
+    for (int b = 0; b < 3; b++) {
+        P->relpos0[b] = hce[b].a;
+        P->orient0[b] = sc > 0 ? rint(hce[3 + b].a * sc) / sc : hce[3 + b].a;
+    }
+}
+
 int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const mfg_opts *O, double *w_out,
               mfg_result *res) {
     models_t MM;
     memset(&MM, 0, sizeof MM);
     if (mfo_model_from_blob(blob0, &MM.M[0])) return -1;
     frame_from_arr(P->frame[0], &MM.F[0]);
-    if (P->family == MFG_BOX) {
+    if (P->family == MFG_BOX || P->family == MFG_CENT) {
         if (!blob1 || mfo_model_from_blob(blob1, &MM.M[1])) return -1;
         frame_from_arr(P->frame[1], &MM.F[1]);
     }
-    const int N = P->N, nx = P->nx, nu = P->nu, nv = nx + nu, ni = P->ni, ne = P->ne;
+    const int N = P->N, nx = P->nx, nu = P->nu, nv = nx + nu, ni = P->ni, ne = P->ne + P->nem;
     const int mb = 2 * nx + nu + ne;
     if (N < 1 || nx > GX || nu > GU || ni > GI || ne > GE || mb > BKMAX) return -2;
     ws_t SS, *S = &SS;
     memset(S, 0, sizeof *S);
-    S->P = P; S->O = O; S->MM = &MM;
-    S->N = N; S->nx = nx; S->nu = nu; S->nv = nv; S->ni = ni; S->ne = ne; S->mb = mb;
+    mfg_ocp PL = *P;  /* local copy: the Centauro targets are set from x_0 */
+    S->P = &PL; S->O = O; S->MM = &MM;
+    S->N = N; S->nx = nx; S->nu = nu; S->nv = nv; S->ni = ni; S->ne = ne; S->mb = mb; S->nes = P->ne;
+    if (P->family == MFG_CENT) cent_targets(&PL, &MM);
     const double h_unused = P->h; (void)h_unused;
 
     /* ---- bounds (IPOPT bound_relax_factor on every non-fixed bound) ---- */
@@ -752,7 +848,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     S->zxL = dal(NX1); S->zxU = dal(NX1); S->zuL = dal(NU); S->zuU = dal(NU); S->vL = dal(NI); S->vU = dal(NI);
     S->tx = dal(NX1); S->tu = dal(NU); S->ts = dal(NI);
     S->l = dal(N); S->gl = dal((size_t)N * nv); S->ci = dal(NI); S->Ji = dal(NI * nv); S->ce = dal(NE);
-    S->Je = dal(NE * nx); S->f = dal((size_t)N * nx); S->Af = dal((size_t)N * nx * nx); S->Bf = dal((size_t)N * nx * nu);
+    S->Je = dal(NE * nv); S->f = dal((size_t)N * nx); S->Af = dal((size_t)N * nx * nx); S->Bf = dal((size_t)N * nx * nu);
     S->W = dal((size_t)N * nv * nv);
     S->dx = dal(NX1); S->du = dal(NU); S->ds = dal(NI); S->dlam = dal((size_t)N * nx); S->dye = dal(NE);
     S->dyi = dal(NI); S->dzxL = dal(NX1); S->dzxU = dal(NX1); S->dzuL = dal(NU); S->dzuU = dal(NU);
@@ -840,8 +936,8 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
                     r += S->gl[k * nv + j];
                     for (int jj = 0; jj < nx; jj++) r += S->Af[(k * nx + jj) * nx + j] * S->lam[k * nx + jj];
                     for (int q = 0; q < ni; q++) r += S->Ji[((size_t)k * ni + q) * nv + j] * S->yi[k * ni + q];
-                    if (EQ_ON(S, k))
-                        for (int e = 0; e < ne; e++) r += S->Je[(k * ne + e) * nx + j] * S->ye[k * ne + e];
+                    for (int e = 0; e < ne; e++)
+                        if (EQ_ON(S, k, e)) r += S->Je[((size_t)k * ne + e) * nv + j] * S->ye[k * ne + e];
                 }
                 r += -S->zxL[i] + S->zxU[i];
                 dinf = fmax(dinf, fabs(r));
@@ -855,6 +951,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
                 double r = S->gl[k * nv + nx + j];
                 for (int jj = 0; jj < nx; jj++) r += S->Bf[(k * nx + jj) * nu + j] * S->lam[k * nx + jj];
                 for (int q = 0; q < ni; q++) r += S->Ji[((size_t)k * ni + q) * nv + nx + j] * S->yi[k * ni + q];
+                for (int e = S->nes; e < ne; e++) r += S->Je[((size_t)k * ne + e) * nv + nx + j] * S->ye[k * ne + e];
                 r += -S->zuL[i] + S->zuU[i];
                 dinf = fmax(dinf, fabs(r));
                 if (hasb(S->ulo[i])) COMP(S->zuL[i], S->u[i] - S->ulo[i]);
@@ -874,8 +971,8 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
                 pinf = fmax(pinf, fabs(S->f[k * nx + j] - S->x[(k + 1) * nx + j]));
                 sum_mult += fabs(S->lam[k * nx + j]); n_mult++;
             }
-            if (EQ_ON(S, k))
-                for (int e = 0; e < ne; e++) {
+            for (int e = 0; e < ne; e++)
+                if (EQ_ON(S, k, e)) {
                     pinf = fmax(pinf, fabs(S->ce[k * ne + e]));
                     sum_mult += fabs(S->ye[k * ne + e]); n_mult++;
                 }
@@ -939,7 +1036,10 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
 #undef SIGG
 
         /* ---- inertia-corrected block factorisation ---- */
-        double dw = 0.0, dc = 0.0, d1 = 0.0;
+        /* delta_c = 1e-8 mu^(1/4) (IPOPT's perturbation of a singular KKT) from the first attempt when
+         * the equality rows are rank deficient by construction (Centauro moment rows at the fixed
+         * node 0: (p_L - p_R) x (F_L - F_R) has rank 2 in F), else only after a zero pivot */
+        double dw = 0.0, dc = P->dc_always ? 1e-8 * pow(mu, 0.25) : 0.0, d1 = 0.0;
         int tier = reg_tier, step_no = 0, factor_ok = 0, tries;
         double reg = (reg_tier == 0) ? 0.0 : reg_last / 3.0;
         if (reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
@@ -1113,11 +1213,11 @@ int mfg_node_derivs(const double *blob0, const double *blob1, const mfg_ocp *P, 
     memset(&MM, 0, sizeof MM);
     if (mfo_model_from_blob(blob0, &MM.M[0])) return -1;
     frame_from_arr(P->frame[0], &MM.F[0]);
-    if (P->family == MFG_BOX) {
+    if (P->family == MFG_BOX || P->family == MFG_CENT) {
         if (!blob1 || mfo_model_from_blob(blob1, &MM.M[1])) return -1;
         frame_from_arr(P->frame[1], &MM.F[1]);
     }
-    const int nx = P->nx, nv = P->nx + P->nu, ni = P->ni, ne = P->ne, no = 1 + ni + ne + nx;
+    const int nx = P->nx, nv = P->nx + P->nu, ni = P->ni, ne = P->ne + P->nem, no = 1 + ni + ne + nx;
     for (int a = 0; a < nv; a++)
         for (int b = a; b < nv; b++) {
             hd hx[GV], hl, hci[GI], hce[GE], hf[GX];

@@ -19,10 +19,14 @@ static void run(const DevModel *M, const DevFrame *F, const GParams &P, const do
     typename FAM::Scratch S;
     std::memset(&S, 0, sizeof S);
     const double *x = xu, *u = xu + D::NX;
+    double yev[D::NET];  // [state rows (NE) | mixed rows (NM)] -> [NEA | NM]
+    for (int i = 0; i < D::NET; i++) yev[i] = 0.0;
+    for (int i = 0; i < D::NE; i++) yev[i] = ye[i];
+    for (int i = 0; i < D::NM; i++) yev[D::NEA + i] = ye[D::NE + i];
     for (int t = 0; t < FAM::PRE; t++) FAM::prepass(M, F, P, x, u, t, S);
-    FAM::seeds(P, u, yi, ye, lam, true, S);
+    FAM::seeds(P, u, yi, yev, lam, true, S);
     for (int t = 0; t < FAM::LANES; t++) FAM::lane(M, F, x, u, yi, t, S);
-    for (int e = 0; e < D::REC; e++) rec[e] = FAM::rec(P, x, u, yi, ye, lam, true, S, e, lref);
+    for (int e = 0; e < D::REC; e++) rec[e] = FAM::rec(P, x, u, yi, yev, lam, true, S, e, lref);
 }
 
 static int frame_of(const Model &m, const char *name) {
@@ -31,7 +35,8 @@ static int frame_of(const Model &m, const char *name) {
     throw std::runtime_error("frame");
 }
 
-// family: 0 box (urdf0, urdf1), 1 chain 6-DOF force+line, 2 chain 6-DOF force+line+thermal.
+// family: 0 box (urdf0, urdf1), 1 chain 6-DOF force+line, 2 chain 6-DOF force+line+thermal,
+// 3 Centauro (urdf0 / urdf1 with frames mass1_ee / mass2_ee; lref = the 6 pose targets).
 // P: GParams filled by the caller (layout shared with the product's ctypes mirror).  Returns the record size.
 extern "C" int fam_node_record(int family, const char *urdf0, const char *urdf1, const char *frame, const GParams *P,
                                const double *xu, const double *yi, const double *ye, const double *lam,
@@ -48,6 +53,15 @@ extern "C" int fam_node_record(int family, const char *urdf0, const char *urdf1,
             F[1] = make_dev_frame(m1, frame_of(m1, frame));
             run<BoxFam>(M, F, *P, xu, yi, ye, lam, lref, rec);
             return BoxFam::D::REC;
+        }
+        if (family == 3) {
+            Model m1 = build_model_from_urdf(urdf1);
+            M[0] = make_dev_model(m0);
+            F[0] = make_dev_frame(m0, frame_of(m0, "mass1_ee"));
+            M[1] = make_dev_model(m1);
+            F[1] = make_dev_frame(m1, frame_of(m1, "mass2_ee"));
+            run<CentauroFam>(M, F, *P, xu, yi, ye, lam, lref, rec);
+            return CentauroFam::D::REC;
         }
         if (family == 1) {
             run<ChainFam<6, 1, 2, false>>(M, F, *P, xu, yi, ye, lam, lref, rec);

@@ -150,4 +150,84 @@ def test_thermal_receding_horizon_matches_oracle(decimals, steps):
         assert all(r_or.status == 0 for _, r_or in ref)
         # the temperatures carried across restarts drop by T_drop at each restart
         w1 = res[1].w[0]
-        np.testing.assert_allclose(w1[3:6], np.asarray(ref[0][0][-6:-3]) - 0.05, atol=1e-9)
+        np.testing.assert_allclose(w1[3:6], np.asarray(ref[0][0][-3:]) - 0.05, atol=1e-9)
+
+
+def test_centauro_device_record_matches_oracle():
+    """C4 node record from the device kernel (k_grec<CentauroFam>) = the oracle's hyper-dual record:
+    tau = ID + J^T F of both 7-DOF arms, relative pose rows, equilibrium (mixed) rows, thermal dynamics,
+    the full Lagrangian Hessian."""
+    rng = np.random.default_rng(5)
+    spec = PR.centauro(N=2)
+    ocp = GOCP(spec)
+    nx, nu, ni, ne, nm = ocp.nx, ocp.nu, ocp.ni, ocp.ne, ocp.nem
+    assert (nx, nu, ni, ne, nm) == (28, 20, 14, 6, 6)
+    q0 = np.asarray(spec["q0"])
+    xu = np.r_[q0 + 0.2 * rng.normal(size=14), 20 + 30 * rng.uniform(size=14), 0.5 * rng.normal(size=14),
+               rng.normal(size=3) * 5 + [0, 0, 49], rng.normal(size=3) * 5 + [0, 0, 49]]
+    yi, ye, lam = 10 * rng.normal(size=ni), rng.normal(size=ne + nm), rng.normal(size=nx)
+    rec = ocp.node_record(xu, yi, ye, lam, line_ref=np.zeros(6))
+    nv = nx + nu
+    vals, jac, H = G.node_derivs(spec, xu, yi, ye, lam)
+    o = 1 + nv + ni + ni * nv
+    ce, Je = rec[o:o + ne], rec[o + ne:o + ne + ne * nx].reshape(ne, nx)
+    o += ne + ne * nx
+    cm, Jm = rec[o:o + nm], rec[o + nm:o + nm + nm * nv].reshape(nm, nv)
+    o += nm + nm * nv
+    W = rec[-nv * nv:].reshape(nv, nv)
+    sc = lambda a: max(1.0, np.abs(a).max())
+    np.testing.assert_allclose(rec[0], vals[0], rtol=1e-12)
+    np.testing.assert_allclose(rec[1:1 + nv], jac[0], atol=1e-11 * sc(jac[0]))
+    np.testing.assert_allclose(rec[1 + nv:1 + nv + ni], vals[1:1 + ni], atol=1e-11 * sc(vals[1:1 + ni]))
+    np.testing.assert_allclose(ce, vals[1 + ni:1 + ni + ne], atol=1e-12)
+    np.testing.assert_allclose(Je, jac[1 + ni:1 + ni + ne, :nx], atol=1e-12)
+    np.testing.assert_allclose(cm, vals[1 + ni + ne:1 + ni + ne + nm], atol=1e-11 * sc(cm))
+    np.testing.assert_allclose(Jm, jac[1 + ni + ne:1 + ni + ne + nm], atol=1e-11 * sc(Jm))
+    np.testing.assert_allclose(rec[o:o + nx], vals[1 + ni + ne + nm:], atol=1e-12 * sc(vals[1 + ni + ne + nm:]))
+    np.testing.assert_allclose(W, H, atol=1e-10 * sc(H))
+
+
+def test_centauro_gpu_matches_oracle_c4():
+    """C4 at the reference's horizon (N = 40, T = 30 s, RepeatedMPCwithThermal.py:86-90) from the IK start:
+    GPU = oracle, and the solution keeps the box balanced and the hands' relative pose."""
+    from tests.test_centauro_cpu import check_solution
+
+    spec = PR.centauro(N=40)
+    ocp = GOCP(spec)
+    kw = dict(u_init=PR.centauro_u_init(spec), max_iter=500, max_soc=4)
+    r = ocp.solve(**kw)
+    w_ref, r_ref = G.solve(spec, **kw)
+    assert int(r.status[0]) == 0 and r_ref.status == 0, (int(r.status[0]), int(r.iters[0]), r_ref.status)
+    assert abs(int(r.iters[0]) - r_ref.iter) <= 2
+    np.testing.assert_allclose(r.w[0], w_ref, atol=1e-6)
+    check_solution(spec, r.w[0])
+
+
+def test_centauro_receding_horizon_gpu_matches_oracle():
+    """The thermal MPC loop of RepeatedMPCwithThermal.py:154-487 (restart x_0 <- x_N with T - 0.05,
+    qd_0 <- qd_{N-1}, 4-decimal rounding, targets rounded to 3 decimals after the first solve, previous
+    solution as warm start) on the GPU, step by step equal to the oracle; the windings heat up."""
+    from mpc_fatigue_amd.mpc import GRecedingHorizon
+
+    N, steps = 20, 3
+    spec = PR.centauro(N=N)
+    # the reference's loop tolerances (tol = constr_viol_tol = 1e-3, RepeatedMPCwithThermal.py:441-445): the
+    # rounded orientation target cannot be met exactly at node 1 (q_1 is fixed by q_0 and qd_0)
+    kw = dict(u_init=PR.centauro_u_init(spec), tol=1e-3, constr_viol_tol=1e-3, max_iter=500, max_soc=4)
+    loop = GRecedingHorizon(spec, restart_spec=dict(spec, target_decimals=3), **kw)
+    x0 = np.r_[spec["q0"], spec["T0"]]
+    res = loop.run(x0[None], steps)
+    g, _ = G.make(spec)
+    nx, nu = g.nx, g.nu
+    x, u, prev = x0, np.zeros(nu), None
+    for s in range(steps):
+        sp = PR.centauro(N=N, q0=x[:14], T0=x[14:], qd0=u[:14], target_decimals=(3 if s else -1))
+        w, r = G.solve(sp, w0=prev, **kw)
+        assert int(res[s].status[0]) == r.status, (s, int(res[s].status[0]), r.status)
+        if r.status == 0:
+            np.testing.assert_allclose(res[s].w[0], w, atol=1e-6, err_msg=f"step {s}")
+        off = nx + (N - 1) * (nu + nx)
+        xN = w[off + nu:off + nu + nx].copy()
+        xN[14:] -= 0.05
+        x, u, prev = np.round(xN, 4), np.round(w[off:off + nu], 4), w
+    assert x[14:].max() > 20.5
