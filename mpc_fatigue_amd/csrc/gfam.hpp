@@ -140,26 +140,38 @@ MF_HD double skew_el(const double *y, int r, int c) {  // [y]x (r, c)
     return c == 0 ? -y[1] : y[0];
 }
 
-// ================================================================ BoxFam (C3)
-struct BoxFam {
-    static constexpr int NJ = 6, NARM = 2, NDIR = 2 * NJ, NM = 2;
-    using D = GDims<12, 18, 18, 1>;
+// ================================================================ BoxFam (C3) / shared fatigue budget (N2)
+// TH: the winding temperatures of the 12 joints as state, x = [q_L, q_R, T (12)], the thermal recursion of
+// Tmodel_library.py:9-41 per joint with that joint's arm torque, and one more slack row: the shared
+// fatigue budget sum_j T_j <= c_hi (build-defined extension of C3; parity unpinned).
+template <bool TH> struct BoxFamT {
+    static constexpr int NJ = 6, NARM = 2, NDIR = 2 * NJ, NM = 2, NQ = 12;
+    using D = GDims<TH ? 2 * NQ : NQ, 18, TH ? 19 : 18, 1>;
+    static constexpr int NX = D::NX;
     static constexpr int LANES = NARM * NDIR;  // derivative lanes per node
     static constexpr int LCOL = GLaneOut<NJ>::LCOL;
+    static constexpr int LREF = 2;             // per-problem data (unused)
     // per-node scratch
     struct Scratch {
         double E[NARM][3], tau[NARM][NJ], seed[NARM][3], d[3], dF[3], eb[3];
+        double cw[NARM][NJ], om[NARM][NJ];     // torque weights of the sweeps, thermal Gauss-Newton weights
         double col[NARM][NDIR][LCOL];
     };
-    // variables: q_L 0-5, q_R 6-11 | qd_L 12-17, qd_R 18-23, F_L 24-26, F_R 27-29
-    // kind: 0 q, 1 qd, 2 F; arm; local index
+    // variables: q_L 0-5, q_R 6-11, (T 12-23) | qd_L, qd_R (NX..NX+11), F_L, F_R (NX+12..NX+17)
+    // kind: 0 q, 1 qd, 2 F, 3 T; arm; local index
     MF_HD static void var(int v, int &kind, int &arm, int &loc) {
-        if (v < 12) { kind = 0; arm = v / 6; loc = v % 6; }
-        else if (v < 24) { kind = 1; arm = (v - 12) / 6; loc = (v - 12) % 6; }
-        else { kind = 2; arm = (v - 24) / 3; loc = (v - 24) % 3; }
+        if (v < NQ) { kind = 0; arm = v / 6; loc = v % 6; }
+        else if (v < NX) { kind = 3; arm = (v - NQ) / 6; loc = (v - NQ) % 6; }
+        else if (v < NX + NQ) { kind = 1; arm = (v - NX) / 6; loc = (v - NX) % 6; }
+        else { kind = 2; arm = (v - NX - NQ) / 3; loc = (v - NX - NQ) % 3; }
     }
+    MF_HD static double ploss(const GParams &P, int j, double tau, double qd) {
+        const double ia = tau / P.ktau[j];
+        return P.Ra * ia * ia + qd * qd / P.Rh;
+    }
+    template <class MA, class FA> MF_HD static void targets(MA, FA, const GParams &, const double *, double *) {}
 
-    // values at (x, u): l, ci, ce, f (line search / slacks).  E: frame points out (may be null)
+    // values at (x, u): l, ci, ce, f (line search / slacks)
     template <class MA, class FA> MF_HD static void values(MA M, FA F, const GParams &P, const double *x, const double *u,
                              const double *, double &l, double *ci, double *ce, double *f) {
         double tL[NJ], tR[NJ], E1[3], E2[3];
@@ -180,16 +192,24 @@ struct BoxFam {
             const double e = 0.5 * (E1[r] + E2[r]) - P.box_pdes[r];
             c += P.w_box * e * e;
         }
-        for (int j = 0; j < 12; j++) {
+        for (int j = 0; j < NQ; j++) {
             c += P.w_qdb * u[j] * u[j];
             f[j] = x[j] + P.h * u[j];
+        }
+        if constexpr (TH) {
+            double sum = 0.0;
+            for (int j = 0; j < NQ; j++) {
+                const double t = j < NJ ? tL[j] : tR[j - NJ];
+                f[NQ + j] = P.th_a * x[NQ + j] + P.th_b * ploss(P, j, t, u[j]);
+                c += P.wT * x[NQ + j] * x[NQ + j];
+                sum += x[NQ + j];
+            }
+            ci[18] = sum;
         }
         l = c;
     }
 
     static constexpr int PRE = NARM;  // pre-pass lanes per node
-    static constexpr int LREF = 2;    // per-problem data (unused)
-    template <class MA, class FA> MF_HD static void targets(MA, FA, const GParams &, const double *, double *) {}
     // pre-pass lane a: frame point E_a and tau_a at the node
     template <class MA, class FA> MF_HD static void prepass(MA M, FA F, const GParams &, const double *x, const double *u,
                               int a, Scratch &S) {
@@ -197,7 +217,8 @@ struct BoxFam {
     }
     // seeds of both arms from the pre-pass: lambda_E = d g / d E_a of the algebraic part
     //   g = w_box |(E1+E2)/2 - p|^2 + ye (|d|^2 - L) + y_m . (d x dF),  d = E1 - E2, dF = F_L - F_R
-    MF_HD static void seeds(const GParams &P, const double *u, const double *yi, const double *ye, const double *,
+    // and the torque weights c = y_tau (+ 2 tau lam_T b Ra / ktau^2 with the thermal state)
+    MF_HD static void seeds(const GParams &P, const double *u, const double *yi, const double *ye, const double *lam,
                             bool eqon, Scratch &S) {
         const double yev = eqon ? ye[0] : 0.0;
         const double *ym = yi + 3;
@@ -212,12 +233,22 @@ struct BoxFam {
             S.seed[0][r] = S.eb[r] + 2.0 * yev * S.d[r] + dFxy[r];
             S.seed[1][r] = S.eb[r] - 2.0 * yev * S.d[r] - dFxy[r];
         }
+        for (int a = 0; a < NARM; a++)
+            for (int j = 0; j < NJ; j++) {
+                double w = 0.0;
+                if constexpr (TH) {
+                    const int i = NJ * a + j;
+                    w = lam[NQ + i] * P.th_b * P.Ra / (P.ktau[i] * P.ktau[i]);
+                }
+                S.om[a][j] = 2.0 * w;
+                S.cw[a][j] = yi[6 + NJ * a + j] + 2.0 * w * S.tau[a][j];
+            }
     }
     // derivative lane t in [0, LANES): arm t / NDIR, direction t % NDIR
-    template <class MA, class FA> MF_HD static void lane(MA M, FA F, const double *x, const double *u, const double *yi,
+    template <class MA, class FA> MF_HD static void lane(MA M, FA F, const double *x, const double *u, const double *,
                            int t, Scratch &S) {
         const int a = t / NDIR, v = t % NDIR;
-        arm_lane<NJ>(M[a], F[a], x + 6 * a, u + 6 * a, u + 12 + 3 * a, yi + 6 + 6 * a, S.seed[a], v, S.col[a][v]);
+        arm_lane<NJ>(M[a], F[a], x + 6 * a, u + 6 * a, u + 12 + 3 * a, S.cw[a], S.seed[a], v, S.col[a][v]);
     }
     // dE_a[c] / d(var) (frame-point Jacobian; zero unless var is a q of arm a)
     MF_HD static double JE(const Scratch &S, int a, int c, int v) {
@@ -225,14 +256,25 @@ struct BoxFam {
         var(v, kind, arm, loc);
         return (kind == 0 && arm == a) ? S.col[a][loc][GLaneOut<NJ>::PFD + c] : 0.0;
     }
+    // d tau_(a, i) / d(var)
+    MF_HD static double dtau(const Scratch &S, int a, int i, int v) {
+        using L = GLaneOut<NJ>;
+        int k, b, l;
+        var(v, k, b, l);
+        if (b != a || k == 3) return 0.0;
+        if (k == 0) return S.col[a][l][L::JT + i];
+        if (k == 1) return S.col[a][NJ + l][L::JT + i];
+        return -S.col[a][i][L::PFD + l];  // d tau_i / d F_c = -dE_c / dq_i
+    }
     // W(r, c) of the Lagrangian Hessian
-    MF_HD static double Wel(const GParams &P, const double *yi, const double *ye, bool eqon, const Scratch &S, int r,
-                            int c) {
+    MF_HD static double Wel(const GParams &P, const double *yi, const double *ye, const double *lam, bool eqon,
+                            const Scratch &S, int r, int c) {
         int kr, ar, lr, kc, ac, lc;
         var(r, kr, ar, lr);
         var(c, kc, ac, lc);
         using L = GLaneOut<NJ>;
         double w = 0.0;
+        if (kr == 3 || kc == 3) return (r == c) ? 2.0 * P.wT : 0.0;  // T enters linearly (plus wT |T|^2)
         // arm sweeps (phi_a = c.tau_a + seed_a . E_a)
         if (ar == ac && !(kr == 2 && kc == 2)) {
             auto colent = [&](int vdir, int kind, int loc) {  // column vdir of arm ar, row (kind, loc)
@@ -243,6 +285,13 @@ struct BoxFam {
             if (kr == 2) w = colent(dc, kr, lr);
             else if (kc == 2) w = colent(dr, kc, lc);
             else w = 0.5 * (colent(dc, kr, lr) + colent(dr, kc, lc));
+        }
+        if constexpr (TH) {  // thermal Gauss-Newton: sum_i om_i dtau_i/dr dtau_i/dc (same arm)
+            if (ar == ac) {
+                double acc = 0.0;
+                for (int i = 0; i < NJ; i++) acc += S.om[ar][i] * dtau(S, ar, i, r) * dtau(S, ar, i, c);
+                w += acc;
+            }
         }
         // algebraic part: J_E^T (d^2 g / dE dE) J_E and the E-F cross terms of the moment rows
         const double yev = eqon ? ye[0] : 0.0;
@@ -258,16 +307,18 @@ struct BoxFam {
             for (int k = 0; k < 3; k++) acc += JE(S, aq, k, vq) * skew_el(yi + 3, k, lf);
             w += sgn * acc;
         }
-        if (r == c && kr == 1) w += 2.0 * P.w_qdb;
+        if (r == c && kr == 1) {
+            w += 2.0 * P.w_qdb;
+            if constexpr (TH) w += lam[NQ + NJ * ar + lr] * P.th_b * 2.0 / P.Rh;
+        }
         return w;
     }
     // record entry e (D offsets)
     MF_HD static double rec(const GParams &P, const double *x, const double *u, const double *yi, const double *ye,
-                            const double *, bool eqon, const Scratch &S, int e, const double *) {
-        using L = GLaneOut<NJ>;
+                            const double *lam, bool eqon, const Scratch &S, int e, const double *) {
         if (e >= D::O_W) {
             const int i = e - D::O_W;
-            return Wel(P, yi, ye, eqon, S, i / D::NV, i % D::NV);
+            return Wel(P, yi, ye, lam, eqon, S, i / D::NV, i % D::NV);
         }
         if (e == D::O_L) {
             double c = 0.0;
@@ -275,7 +326,10 @@ struct BoxFam {
                 const double v = 0.5 * (S.E[0][r] + S.E[1][r]) - P.box_pdes[r];
                 c += P.w_box * v * v;
             }
-            for (int j = 0; j < 12; j++) c += P.w_qdb * u[j] * u[j];
+            for (int j = 0; j < NQ; j++) {
+                c += P.w_qdb * u[j] * u[j];
+                if constexpr (TH) c += P.wT * x[NQ + j] * x[NQ + j];
+            }
             return c;
         }
         if (e < D::O_CI) {  // grad l
@@ -287,7 +341,8 @@ struct BoxFam {
                 for (int c = 0; c < 3; c++) acc += JE(S, a, c, v) * S.eb[c];
                 return acc;
             }
-            return k == 1 ? 2.0 * P.w_qdb * u[v - 12] : 0.0;
+            if (k == 3) return 2.0 * P.wT * x[v];
+            return k == 1 ? 2.0 * P.w_qdb * u[v - NX] : 0.0;
         }
         if (e < D::O_JI) {  // c_in values
             const int r = e - D::O_CI;
@@ -299,12 +354,17 @@ struct BoxFam {
                 cross3(m, S.d, S.dF);
                 return m[r - 3];
             }
-            return r < 12 ? S.tau[0][r - 6] : S.tau[1][r - 12];
+            if (r < 18) return r < 12 ? S.tau[0][r - 6] : S.tau[1][r - 12];
+            double sum = 0.0;  // shared fatigue budget
+            for (int j = 0; j < NQ; j++) sum += x[NQ + j];
+            return sum;
         }
         if (e < D::O_CE) {  // d c_in
             const int i = e - D::O_JI, r = i / D::NV, v = i % D::NV;
             int k, a, l;
             var(v, k, a, l);
+            if (r == 18) return k == 3 ? 1.0 : 0.0;
+            if (k == 3) return 0.0;
             if (r < 3) {  // F_L + F_R - (0, 0, m g), rows (z, x, y)
                 const int comp = r == 0 ? 2 : r - 1;
                 return (k == 2 && l == comp) ? 1.0 : 0.0;
@@ -320,9 +380,7 @@ struct BoxFam {
                 return 0.0;
             }
             const int ta = r < 12 ? 0 : 1, ti = (r - 6) % 6;
-            if (a != ta) return 0.0;
-            if (k == 2) return -S.col[ta][ti][L::PFD + l];  // d tau_i / d F_c = -dE_c / dq_i
-            return S.col[ta][k == 0 ? l : NJ + l][L::JT + ti];
+            return dtau(S, ta, ti, v);
         }
         if (e < D::O_JE) {  // c_eq
             return S.d[0] * S.d[0] + S.d[1] * S.d[1] + S.d[2] * S.d[2] - P.box_L;
@@ -333,18 +391,29 @@ struct BoxFam {
             for (int c = 0; c < 3; c++) acc += 2.0 * S.d[c] * (JE(S, 0, c, v) - JE(S, 1, c, v));
             return acc;
         }
-        if (e < D::O_A) {  // f = q + h qd
+        if (e < D::O_A) {  // f = [q + h qd, a T + b Ploss]
             const int j = e - D::O_F;
-            return x[j] + P.h * u[j];
+            if (j < NQ) return x[j] + P.h * u[j];
+            const int t = j - NQ;
+            return P.th_a * x[j] + P.th_b * ploss(P, t, S.tau[t / NJ][t % NJ], u[t]);
         }
         if (e < D::O_B) {
-            const int i = e - D::O_A;
-            return (i / D::NX == i % D::NX) ? 1.0 : 0.0;
+            const int i = e - D::O_A, r = i / NX, c = i % NX;
+            if (r < NQ) return r == c ? 1.0 : 0.0;
+            const int t = r - NQ;
+            if (c >= NQ) return c == r ? P.th_a : 0.0;
+            return P.th_b * 2.0 * P.Ra * S.tau[t / NJ][t % NJ] / (P.ktau[t] * P.ktau[t]) * dtau(S, t / NJ, t % NJ, c);
         }
         const int i = e - D::O_B, r = i / D::NU, c = i % D::NU;
-        return (c == r) ? P.h : 0.0;
+        if (r < NQ) return (c == r) ? P.h : 0.0;
+        const int t = r - NQ;
+        double a = P.th_b * 2.0 * P.Ra * S.tau[t / NJ][t % NJ] / (P.ktau[t] * P.ktau[t]) * dtau(S, t / NJ, t % NJ, NX + c);
+        if (c == t) a += P.th_b * 2.0 * u[t] / P.Rh;
+        return a;
     }
 };
+using BoxFam = BoxFamT<false>;
+using BoxThermFam = BoxFamT<true>;
 
 // ================================================================ ChainFam (C1, C2, thermal)
 template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {

@@ -1051,13 +1051,14 @@ using namespace mf;
     } while (0)
 
 // the kernel instantiations (family, dims) and their dispatch
-enum GKind { GK_BOX = 0, GK_CH6F = 1, GK_CH6FT = 2, GK_CH3 = 3, GK_CH3T = 4, GK_CENT = 5 };
+enum GKind { GK_BOX = 0, GK_CH6F = 1, GK_CH6FT = 2, GK_CH3 = 3, GK_CH3T = 4, GK_CENT = 5, GK_BOXT = 6 };
 using FamBox = BoxFam;
 using FamCh6F = ChainFam<6, 1, 2, false>;
 using FamCh6FT = ChainFam<6, 1, 2, true>;
 using FamCh3 = ChainFam<3, 0, 0, false>;
 using FamCh3T = ChainFam<3, 0, 0, true>;
 using FamCent = CentauroFam;
+using FamBoxT = BoxThermFam;
 
 struct mf_gproblem {
     mf_model *m0 = nullptr, *m1 = nullptr;
@@ -1197,6 +1198,7 @@ static int gdispatch_solve(mf_gproblem *p, int batch, const double *x0, const do
         case GK_CH3: return gsolve_core<FamCh3>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
         case GK_CH3T: return gsolve_core<FamCh3T>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
         case GK_CENT: return gsolve_core<FamCent>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+        case GK_BOXT: return gsolve_core<FamBoxT>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
     }
     return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }
@@ -1221,7 +1223,7 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
         if (!m1) return capi_fail(MF_ERR_ARG, "the box family needs two models");
         if ((e = capi_model_dev(m1, &dM1, &h1))) return e;
         if (n0 != 6 || (int)h1->joints.size() != 6) return capi_fail(MF_ERR_UNSUPPORTED, "box family: two 6-joint arms");
-        kind = GK_BOX;
+        kind = spec->thermal ? GK_BOXT : GK_BOX;
     } else if (spec->family == MF_FAM_CENTAURO) {
         if (!m1) return capi_fail(MF_ERR_ARG, "the Centauro family needs two models");
         if ((e = capi_model_dev(m1, &dM1, &h1))) return e;
@@ -1257,6 +1259,7 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
         case GK_CH3: dims_of<FamCh3>(p->nx, p->nu, p->ni, p->ne); break;
         case GK_CH3T: dims_of<FamCh3T>(p->nx, p->nu, p->ni, p->ne); break;
         case GK_CENT: dims_of<FamCent>(p->nx, p->nu, p->ni, p->ne); break;
+        case GK_BOXT: dims_of<FamBoxT>(p->nx, p->nu, p->ni, p->ne); break;
     }
     const int N = spec->N;
     int rc = capi_frame_dev(m0, spec->frame0, &p->dF0);
@@ -1281,7 +1284,7 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
     memcpy(P.x_lo, spec->x_lo, sizeof P.x_lo);
     memcpy(P.x_hi, spec->x_hi, sizeof P.x_hi);
     P.target_decimals = spec->target_decimals;
-    if (kind == GK_BOX) { P.force_from = 12; P.tier1_from = P.tier1_to = 0; }
+    if (kind == GK_BOX || kind == GK_BOXT) { P.force_from = 12; P.tier1_from = P.tier1_to = 0; }
     else if (kind == GK_CENT) {
         // the moment rows at the fixed node 0 have rank 2 in F: IPOPT sees a singular KKT every
         // iteration and perturbs it with delta_c; the solver does so from the first factorisation
@@ -1433,6 +1436,7 @@ extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {
         case GK_CH3: return gdual_core<FamCh3>(p, b, out);
         case GK_CH3T: return gdual_core<FamCh3T>(p, b, out);
         case GK_CENT: return gdual_core<FamCent>(p, b, out);
+        case GK_BOXT: return gdual_core<FamBoxT>(p, b, out);
     }
     return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }
@@ -1454,6 +1458,7 @@ extern "C" int mf_gnode_record(mf_gproblem *p, const double *xu, const double *y
         case GK_CH3: return grec_core<FamCh3>(p, xu, yi, yv, lam, lr, rec);
         case GK_CH3T: return grec_core<FamCh3T>(p, xu, yi, yv, lam, lr, rec);
         case GK_CENT: return grec_core<FamCent>(p, xu, yi, yv, lam, lr, rec);
+        case GK_BOXT: return grec_core<FamBoxT>(p, xu, yi, yv, lam, lr, rec);
     }
     return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }

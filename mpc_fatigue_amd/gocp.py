@@ -56,8 +56,14 @@ def bounds(spec: dict, n: int) -> GBounds:
         u_lo = np.hstack([np.tile(np.asarray(spec["qd_lo"], float), (N, 1)), np.full((N, 6), -INF)])
         u_hi = np.hstack([np.tile(np.asarray(spec["qd_hi"], float), (N, 1)), np.full((N, 6), INF)])
         u_lo[0, :12] = u_hi[0, :12] = np.asarray(spec["qd0"], float)
-        return GBounds(np.asarray(spec["q_lo"], float), np.asarray(spec["q_hi"], float), u_lo, u_hi, c_lo, c_hi,
-                       np.asarray(spec["q0"], float))
+        x_lo, x_hi = np.asarray(spec["q_lo"], float), np.asarray(spec["q_hi"], float)
+        x0 = np.asarray(spec["q0"], float)
+        if spec.get("thermal", False):  # shared fatigue budget (problems.box_shared_fatigue)
+            x_lo, x_hi = np.r_[x_lo, np.full(12, spec["T_lo"])], np.r_[x_hi, np.full(12, spec["T_hi"])]
+            x0 = np.r_[x0, np.broadcast_to(np.asarray(spec["T0"], float), (12,))]
+            c_lo = np.hstack([c_lo, np.full((N, 1), -INF)])
+            c_hi = np.hstack([c_hi, np.full((N, 1), spec["T_budget"])])
+        return GBounds(x_lo, x_hi, u_lo, u_hi, c_lo, c_hi, x0)
     nf = spec["nf"]
     x_lo = np.broadcast_to(np.asarray(spec["q_lo"], float), (n,))
     x_hi = np.broadcast_to(np.asarray(spec["q_hi"], float), (n,))
@@ -104,6 +110,12 @@ class GOCP:
         elif box:
             g.box_mg, g.box_L, g.w_box, g.w_qd = spec["box_mg"], spec["box_L"], spec["w_box"], spec["w_qd"]
             g.box_pdes[:] = list(spec["p_des"])
+            if spec.get("thermal", False):
+                g.thermal, g.wT = 1, spec.get("wT", 0.0)
+                g.th_a, g.th_b, g.Ra, g.Rh = spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+                kt = np.zeros(_lib.MF_MAX_JOINTS)
+                kt[:12] = spec["ktau"]
+                g.ktau[:] = list(kt)
         else:
             g.nf, g.use_line = spec["nf"], int(spec["use_line"])
             fd = np.zeros(9)

@@ -324,3 +324,17 @@ def centauro_u_init(spec: dict) -> np.ndarray:
     """Initial controls of the first Centauro solve: qd = 0, each hand carrying half the box,
     F = (0, 0, m g / 2) -- the reference's sol0 (RepeatedMPCwithThermal.py:148-151)."""
     return np.r_[np.zeros(14), [0.0, 0.0, spec["box_mg"] / 2] * 2]
+
+
+def box_shared_fatigue(N: int = 100, T0=60.0, T_hi: float = 80.0, budget_mean: float = 60.1, **kw) -> dict:
+    """C3 "shared fatigue budget" (BASELINE config 3; build-defined, no reference counterpart):
+    the dual-arm box of box_dual with the winding temperature of all 12 joints as state (the a8 recursion of
+    Tmodel_library.py:9-41 / RepeatedMPCwithThermal.py:371-376, h = T / N, kτ = the first six entries of the
+    reference table for each arm), T in [0, T_hi], and one budget row per node shared by both arms:
+    sum_j T_j <= 12 budget_mean."""
+    sp = box_dual(N=N, **kw)
+    a, b = thermal_coeffs(sp["h"])
+    sp.update(name="box_shared_fatigue", thermal=True, th_a=a, th_b=b, Ra=TH_RA, Rh=TH_RH,
+              ktau=list(KTAU14[:6]) * 2, wT=0.0, T0=list(np.broadcast_to(np.asarray(T0, float), (12,))),
+              T_lo=0.0, T_hi=T_hi, T_budget=12.0 * budget_mean)
+    return sp

@@ -48,7 +48,8 @@ int frame_of(const Model &m, const char *name) {
 }
 }  // namespace
 
-// family: 0 box, 1 chain 6-DOF force + line, 2 the same with thermal state, 3 Centauro (two 7-DOF arms)
+// family: 0 box, 1 chain 6-DOF force + line, 2 the same with thermal state, 3 Centauro (two 7-DOF arms),
+// 4 box with thermal state and shared fatigue budget
 extern "C" void *mfc_create(int family, const char *urdf0, const char *urdf1, const char *frame0, const char *frame1,
                             const GParams *P) {
     try {
@@ -57,7 +58,7 @@ extern "C" void *mfc_create(int family, const char *urdf0, const char *urdf1, co
         Model m0 = build_model_from_urdf(urdf0);
         c->M[0] = make_dev_model(m0);
         c->F[0] = make_dev_frame(m0, frame_of(m0, frame0));
-        if (family == 0 || family == 3) {
+        if (family == 0 || family == 3 || family == 4) {
             Model m1 = build_model_from_urdf(urdf1);
             c->M[1] = make_dev_model(m1);
             c->F[1] = make_dev_frame(m1, frame_of(m1, frame1));
@@ -82,6 +83,7 @@ extern "C" int mfc_node(void *ctx, const double *xu, const double *yi, const dou
         case 1: return record<ChainFam<6, 1, 2, false>>(c, xu, yi, ye, lam, lref, eqon, rec);
         case 2: return record<ChainFam<6, 1, 2, true>>(c, xu, yi, ye, lam, lref, eqon, rec);
         case 3: return record<CentauroFam>(c, xu, yi, ye, lam, lref, eqon, rec);
+        case 4: return record<BoxThermFam>(c, xu, yi, ye, lam, lref, eqon, rec);
     }
     return -5;
 }
@@ -102,6 +104,7 @@ extern "C" int mfc_values(void *ctx, const double *x, const double *u, const dou
         case 1: return values<ChainFam<6, 1, 2, false>>(c, x, u, lref, l, ci, ce, f);
         case 2: return values<ChainFam<6, 1, 2, true>>(c, x, u, lref, l, ci, ce, f);
         case 3: return values<CentauroFam>(c, x, u, lref, l, ci, ce, f);
+        case 4: return values<BoxThermFam>(c, x, u, lref, l, ci, ce, f);
     }
     return -5;
 }

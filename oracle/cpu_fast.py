@@ -49,6 +49,12 @@ def gparams(spec: dict) -> GParams:
     if spec.get("family") == "box":
         g.box_mg, g.box_L, g.w_box, g.w_qdb = spec["box_mg"], spec["box_L"], spec["w_box"], spec["w_qd"]
         g.box_pdes[:] = list(spec["p_des"])
+        if spec.get("thermal", False):
+            g.thermal, g.th_a, g.th_b, g.Ra, g.Rh = 1, spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+            g.wT = spec.get("wT", 0.0)
+            kt = np.zeros(16)
+            kt[:12] = spec["ktau"]
+            g.ktau[:] = list(kt)
     elif spec.get("family") == "centauro":
         g.box_mg, g.w_box, g.w_qdb, g.wF = spec["box_mg"], spec["w_box"], spec["w_qd"], spec["wF"]
         g.box_pdes[:] = list(spec["p_des"])
@@ -90,7 +96,7 @@ def lib():
 
 def family_code(spec: dict) -> int:
     if spec.get("family") == "box":
-        return 0
+        return 4 if spec.get("thermal", False) else 0
     if spec.get("family") == "centauro":
         return 3
     if spec["nf"] != 1 or not spec["use_line"]:

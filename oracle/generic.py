@@ -128,8 +128,9 @@ def make(spec: dict):
         g.eq_from = 1
     elif fam == "box":
         n = 12
+        th = bool(spec.get("thermal", False))
         g.family = MFG_BOX
-        g.nx, g.nu, g.ni, g.ne = n, n + 6, 6 + n, 1
+        g.nx, g.nu, g.ni, g.ne = (2 * n if th else n), n + 6, 6 + n + (1 if th else 0), 1
         g.force_from, g.tier1_from, g.tier1_to = n, 0, 0
         for a, m in enumerate(ms):
             g.frame[a][:] = list(O.frame_arr(m, spec["frame"]))
@@ -141,6 +142,18 @@ def make(spec: dict):
         tol = spec["pos_toll"]
         c_lo = np.hstack([np.full((N, 6), -tol), np.asarray(spec["tau_lo"], float)])
         c_hi = np.hstack([np.full((N, 6), tol), np.asarray(spec["tau_hi"], float)])
+        if th:
+            g.thermal = 1
+            g.th_a, g.th_b, g.Ra, g.Rh = spec["th_a"], spec["th_b"], spec["Ra"], spec["Rh"]
+            kt = np.zeros(MJ)
+            kt[:n] = spec["ktau"]
+            g.ktau[:] = list(kt)
+            g.wT = spec.get("wT", 0.0)
+            x_lo = np.r_[x_lo, np.full(n, spec["T_lo"])]
+            x_hi = np.r_[x_hi, np.full(n, spec["T_hi"])]
+            x0 = np.r_[x0, np.broadcast_to(np.asarray(spec["T0"], float), (n,))]
+            c_lo = np.hstack([c_lo, np.full((N, 1), -INF)])
+            c_hi = np.hstack([c_hi, np.full((N, 1), spec["T_budget"])])
         u_lo = np.hstack([np.tile(np.asarray(spec["qd_lo"], float), (N, 1)), np.full((N, 6), -INF)])
         u_hi = np.hstack([np.tile(np.asarray(spec["qd_hi"], float), (N, 1)), np.full((N, 6), INF)])
         u_lo[0, :n] = u_hi[0, :n] = np.asarray(spec["qd0"], float)

@@ -244,6 +244,22 @@ static void node_hd(const mfg_ocp *P, const models_t *MM, const hd *xu, hd *l, h
         c = add(c, muls(mul(u[j], u[j]), P->w_qd));
         f[j] = add(xu[j], muls(u[j], P->h));
     }
+    if (P->thermal) {
+        /* shared fatigue budget (build-defined extension of C3): the winding temperature of
+         * each of the 12 joints as state (Tmodel_library.py:9-41 with that joint's arm torque) and one slack
+         * row sum_j T_j <= budget */
+        const hd *T = xu + 2 * na;
+        hd sum = K(0);
+        for (int j = 0; j < 2 * na; j++) {
+            hd t = j < na ? tL[j] : tR[j - na];
+            hd ia = muls(t, 1.0 / P->ktau[j]);
+            hd pl = add(muls(mul(ia, ia), P->Ra), muls(mul(u[j], u[j]), 1.0 / P->Rh));
+            f[2 * na + j] = add(muls(T[j], P->th_a), muls(pl, P->th_b));
+            if (P->wT != 0.0) c = add(c, muls(mul(T[j], T[j]), P->wT));
+            sum = add(sum, T[j]);
+        }
+        ci[6 + 2 * na] = sum;
+    }
     *l = c;
 }
 

@@ -54,6 +54,13 @@ extern "C" int fam_node_record(int family, const char *urdf0, const char *urdf1,
             run<BoxFam>(M, F, *P, xu, yi, ye, lam, lref, rec);
             return BoxFam::D::REC;
         }
+        if (family == 4) {
+            Model m1 = build_model_from_urdf(urdf1);
+            M[1] = make_dev_model(m1);
+            F[1] = make_dev_frame(m1, frame_of(m1, frame));
+            run<BoxThermFam>(M, F, *P, xu, yi, ye, lam, lref, rec);
+            return BoxThermFam::D::REC;
+        }
         if (family == 3) {
             Model m1 = build_model_from_urdf(urdf1);
             M[0] = make_dev_model(m0);

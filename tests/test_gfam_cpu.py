@@ -130,3 +130,11 @@ def test_centauro_record_matches_oracle(fam, seed):
     xu = np.r_[q0 + 0.2 * rng.normal(size=14), 20 + 30 * rng.uniform(size=14), 0.5 * rng.normal(size=14),
                rng.normal(size=3) * 5 + [0, 0, 49], rng.normal(size=3) * 5 + [0, 0, 49]]
     compare(fam, 3, spec, xu, 28, 20, 14, 6, seed=seed, nm=6)
+
+
+@pytest.mark.parametrize("k", [0, 30])
+def test_box_shared_fatigue_record_matches_oracle(fam, golden, k):
+    """N2 node (dual-arm box + winding temperatures of the 12 joints + the shared budget row)."""
+    g, _ = golden["G1_box_N50"]
+    xu = np.r_[g[k * 30:k * 30 + 12], 60.0 + np.arange(12.0), g[k * 30 + 12:k * 30 + 30]]
+    compare(fam, 4, PR.box_shared_fatigue(N=1), xu, 24, 18, 19, 1, seed=k)

@@ -231,3 +231,23 @@ def test_centauro_receding_horizon_gpu_matches_oracle():
         xN[14:] -= 0.05
         x, u, prev = np.round(xN, 4), np.round(w[off:off + nu], 4), w
     assert x[14:].max() > 20.5
+
+
+def test_box_shared_fatigue_gpu_matches_oracle(golden):
+    """C3 at N = 100 with the shared fatigue budget (BASELINE config 3; build-defined, parity against the
+    oracle only): the winding temperatures of all 12 joints as state, one budget row per node; the
+    homotopy solve on the GPU equals the oracle's, and the budget and the temperature bounds hold."""
+    g, _ = golden["G1_box_N50"]
+    spec = PR.box_shared_fatigue(N=100, q0=g[:12])
+    ocp = GOCP(spec)
+    assert (ocp.nx, ocp.nu, ocp.ni, ocp.ne) == (24, 18, 19, 1)
+    r, stages = ocp.solve_box()
+    assert all(int(s.status[0]) == 0 for s in stages), [(int(s.status[0]), int(s.iters[0])) for s in stages]
+    w_or = None
+    for tol in PR.box_homotopy_tolerances():
+        w_or, ro = G.solve(dict(spec, pos_toll=tol), w0=w_or, u_init=PR.box_u_init(spec), max_iter=1000, max_soc=4)
+    assert ro.status == 0
+    # states (q and T) agree; the split of the forces between the hands is weakly determined (as in C3)
+    np.testing.assert_allclose(ocp.q_traj(r.w[0]), ocp.q_traj(w_or), atol=1e-6)
+    X = ocp.q_traj(r.w[0])
+    assert (X[:, 12:].sum(1) <= spec["T_budget"] + 1e-6).all() and (X[:, 12:] <= spec["T_hi"] + 1e-6).all()
