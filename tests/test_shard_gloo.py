@@ -58,3 +58,61 @@ def test_gather_solutions_gloo(world):
     assert W.shape == (8 * world, 5)
     np.testing.assert_array_equal(W.reshape(-1), np.arange(8 * world * 5))
     assert S == [r for r in range(world) for _ in range(8)]
+
+
+def _solve_worker(rank, world, port, q):
+    """shard -> solve (the oracle stands in for the device on this CPU test) -> gather, the bench's N > 1
+    data flow (bench.py: rank r solves horizons [lo, hi) of the global batch, RCCL gather to rank 0)."""
+    import numpy as np
+
+    from mpc_fatigue_amd import problems as PR
+    from oracle import oracle as O
+    from oracle import pin_np as P
+    from oracle.urdf_np import load_urdf_file
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, total = 8, 2 * world
+    spec = PR.pilz6_bench(N=N)
+    ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
+    Q0 = PR.pilz6_batch_q0(total, seed=0)
+    lo, hi = shard_range(total, world, rank)
+    specs = [PR.pilz6_bench(N=N, q0=Q0[i], line_ref=P.forward_kinematics(ref, Q0[i], "prbt_link_5")[0][:2])
+             for i in range(lo, hi)]
+    w, R = O.solve_batch(ref, specs, nthreads=1, tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1,
+                         F_init=PR.BENCH_F_INIT)
+    W, S = gather_solutions(torch.from_numpy(np.ascontiguousarray(w)),
+                            torch.tensor([r.status for r in R], dtype=torch.int32), rank, world)
+    if rank == 0:
+        q.put((W.numpy().tolist(), S.numpy().tolist()))
+    dist.destroy_process_group()
+
+
+def test_shard_solve_gather_equals_single_process():
+    import numpy as np
+
+    from mpc_fatigue_amd import problems as PR
+    from oracle import oracle as O
+    from oracle import pin_np as P
+    from oracle.urdf_np import load_urdf_file
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_solve_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    W, S = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    N, total = 8, 2 * world
+    spec = PR.pilz6_bench(N=N)
+    ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
+    Q0 = PR.pilz6_batch_q0(total, seed=0)
+    specs = [PR.pilz6_bench(N=N, q0=q0, line_ref=P.forward_kinematics(ref, q0, "prbt_link_5")[0][:2]) for q0 in Q0]
+    w1, R1 = O.solve_batch(ref, specs, nthreads=1, tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1,
+                           F_init=PR.BENCH_F_INIT)
+    np.testing.assert_array_equal(np.array(W), w1)  # same horizons in the same order, bit for bit
+    assert S == [r.status for r in R1]
