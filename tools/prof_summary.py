@@ -1,4 +1,6 @@
-"""Summarise a rocprofv3 --kernel-trace --stats database into profiles/ (markdown)."""
+"""Summarise a rocprofv3 --kernel-trace --stats output (the sqlite database, or the kernel_stats.csv of
+--output-format csv) into profiles/ (markdown)."""
+import csv
 import glob
 import sqlite3
 import sys
@@ -6,8 +8,12 @@ import sys
 
 def main(db_glob: str, out: str, title: str):
     db = sorted(glob.glob(db_glob, recursive=True))[0]
-    c = sqlite3.connect(db)
-    rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
+    if db.endswith(".csv"):
+        rows = [(r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]) / 1e3, float(r["AverageNs"]) / 1e3,
+                 float(r["Percentage"])) for r in csv.DictReader(open(db))]
+    else:
+        c = sqlite3.connect(db)
+        rows = list(c.execute("select name, total_calls, total_duration, average, percentage from top_kernels"))
     with open(out, "w") as f:
         f.write(f"# {title}\n\nSource: `{db}` (rocprofv3 --kernel-trace --stats), durations in microseconds.\n\n")
         f.write("| kernel | calls | total us | avg us | % |\n|---|---|---|---|---|\n")
