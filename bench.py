@@ -94,6 +94,8 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="horizons in the CPU sample (0: 4 per thread)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU runs (median reported)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1024-shard and single-problem figures")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="independent steps in flight (own workspace, stream and host thread each)")
     args = ap.parse_args()
 
     import torch
@@ -136,21 +138,45 @@ def main() -> int:
     ptrs = {k: v.data_ptr() for k, v in out.items()}
     opts = dict(tol=1e-8, constr_viol_tol=1e-8, max_iter=args.max_iter, mu_init=0.1, F_init=PR.BENCH_F_INIT)
 
-    def step():
-        ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), hi - lo, ptrs, stream=stream.cuda_stream, **opts)
-        if world > 1:
-            gather_solutions(out["w"], out["status"], rank, world)
-
-    for _ in range(args.warmup):
-        step()
+    # Steps in flight: consecutive steps are independent batched solves, each on its own solver
+    # workspace and HIP stream, driven by its own host thread (the solve's host loop polls its
+    # stream), so the iteration tail of one step -- few horizons left, latency-bound kernels --
+    # overlaps the bulk of the next.  Every step still solves the whole batch.
+    inflight = max(1, args.inflight)
+    slots = [(ocp, stream, out, ptrs)]
+    for _ in range(inflight - 1):
+        ob = {k: torch.empty_like(v) for k, v in out.items()}
+        slots.append((OCP(spec), torch.cuda.Stream(dev), ob, {k: v.data_ptr() for k, v in ob.items()}))
     torch.cuda.synchronize(dev)
-    ocp.timing(True)
+
+    def solve_on(i):
+        torch.cuda.set_device(dev)  # the HIP device is per host thread
+        o, st, ob, pt = slots[i]
+        o.solve_dev(q0.data_ptr(), lref.data_ptr(), hi - lo, pt, stream=st.cuda_stream, **opts)
+        st.synchronize()
+
+    def run_steps(K):
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(inflight) as ex:
+            futs = []
+            for s_ in range(K + inflight):
+                if s_ >= inflight:  # step s_ - inflight done: its slot is free (gather its solutions)
+                    futs[s_ - inflight].result()
+                    if world > 1:
+                        _, _, ob, _ = slots[(s_ - inflight) % inflight]
+                        gather_solutions(ob["w"], ob["status"], rank, world)
+                if s_ < K:
+                    futs.append(ex.submit(solve_on, s_ % inflight))
+
+    run_steps(max(args.warmup, inflight))  # every slot warm (workspace allocated)
+    torch.cuda.synchronize(dev)
+    if inflight == 1:
+        ocp.timing(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -168,12 +194,21 @@ def main() -> int:
     value = converged * args.steps / elapsed
 
     # ---- node-evaluation kernel vs its HBM roofline; HIP events on the solve stream
+    # With steps in flight the per-kernel HIP-event durations of the timed region include the other
+    # step's kernels running beside them; the kernel figures then come from one more step of the same
+    # batch solved alone right after the timed region (same solver, same iterations).
+    timing_steps = args.steps
+    if inflight > 1:
+        ocp.timing(True)
+        solve_on(0)
+        torch.cuda.synchronize(dev)
+        timing_steps = 1
     stats = ocp.kernel_stats()
     trace = ocp.trace()
     ocp.timing(False)
     ev_ms, ev_launches = stats["k_eval_node"]
     per_launch_ms = ev_ms / max(1, ev_launches)
-    total_bytes = NODE_BYTES * float(node_evals.item()) * args.steps  # this rank's node evaluations
+    total_bytes = NODE_BYTES * float(node_evals.item()) * timing_steps  # this rank's node evaluations
     bytes_per_launch = total_bytes / max(1, ev_launches)
     achieved = total_bytes / (ev_ms / 1e3) / 1e9
     traffic, fp64 = None, None
@@ -203,6 +238,9 @@ def main() -> int:
         "launch_note": ("one k_eval_node launch = the solver's phase 0: k_eval_node<..,0> (q directions) then "
                         "k_eval_node<..,1> (qd directions) on one stream; rocprofv3 lists the two, their averages "
                         "sum to avg_launch_ms. Bytes: SURVEY.md s.8(d) 952 B per running node evaluation"),
+        "timing": ("HIP events over the timed region" if inflight == 1 else
+                   f"HIP events over one step of the same batch solved alone after the timed region ({inflight} steps "
+                   "in flight in the timed region share the GPU, which would inflate every kernel's duration)"),
     }
     # iteration tail: per 4-iteration chunk, problems running at its start and its GPU time (last step)
     tr_ms = trace["ms"]
@@ -222,6 +260,7 @@ def main() -> int:
                    "parallelism": f"dp{world} (independent horizons; RCCL gather of solutions)",
                    "converged_per_step": converged, "converged_frac": converged / gB,
                    "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
+                   "steps_in_flight": inflight,
                    "tol": opts["tol"]},
         "roofline": roofline,
         "tail": tail_rec,
