@@ -76,7 +76,13 @@ template <class T> MF_HD void rodrigues_rows(T *R, const T *A, const double *ax,
 // em.joint(i, tau_i, dphi/dq_i, dphi/dqd_i) during the reverse sweep (i = NJ-1 .. 0).
 // ADJ = false: values only (tau, p_f), the same arithmetic without the adjoint
 // statements (used by the line search and the initial slacks).
-template <class TP, class TV, int NJ, bool ADJ = true, class In, class Emit>
+// GQ = false: no q-gradient (em.joint gets gq = 0, em.force is not called).  The gradient in qd
+// needs only the adjoints of the velocity / acceleration recurrences (w_bar, dw_bar, a_bar) and
+// of the wrench (M_bar = Lz, f_bar = Loz); the geometric adjoints (z_bar, o_bar, the com and
+// frame-point adjoints, Gamma, Obar) feed d phi / dq alone.  A lane of a qd direction whose
+// caller needs only the qd rows of its Hessian column (the q rows follow from the q lanes by
+// symmetry; the force row is identically zero: d phi / dF does not depend on qd) runs GQ = false.
+template <class TP, class TV, int NJ, bool ADJ = true, bool GQ = true, class In, class Emit>
 MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &in, const double *Fw, const double *c,
                         const double *yl, Emit &em) {
     TP R[9], o[3], Lz[3], Loz[3];
@@ -209,14 +215,14 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
         if constexpr (ADJ) {
         // ---- adjoints of link i's quantities (M_bar = Lz, f_bar = Loz)
         TV zb[3], ob[3], cwb[3];
-        {
+        if constexpr (GQ) {
             TV FxO[3], ZxF[3];
             cross3(FxO, Ft, o);
             cross3(ZxF, z, Ft);
 #pragma unroll
             for (int k = 0; k < 3; k++) { zb[k] = (Mt[k] + FxO[k]) * c[i]; ob[k] = ZxF[k] * c[i]; }
         }
-        if (i == fp) {
+        if (GQ && i == fp) {
             TP pfb[3], g1[3], t1[3];
             cross3(pfb, Lz, Fw);
 #pragma unroll
@@ -229,7 +235,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
 #pragma unroll
             for (int k = 0; k < 3; k++) { G[k] += t1[k]; Ob[k] += pfb[k]; }
         }
-        cross3(cwb, f, Lz);
+        if constexpr (GQ) cross3(cwb, f, Lz);
         TP ft[3];
         {
             TP t1[3];
@@ -253,6 +259,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
                 wb[k] += vxl[k] + u2[k] + (ft[k] * wr + r[k] * fw - 2.0 * fr * w[k]) * m;
                 ab[k] += ft[k] * m;
             }
+            if constexpr (GQ) {
             TV r1[3], r2[3], r3[3], r4[3], fxd[3];
             cross3(r1, v1, Lz);
             cross3(r2, u1, dw);
@@ -266,6 +273,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
                 cwb[k] += rb;
                 ob[k] -= rb;
             }
+            }  // GQ
         }
         // ---- recurrences of joint i: w_i = w_p + zq, dw_i = dw_p + w_p x zq, a_i = a_p + dw_p x d + w_p x (w_p x d)
         TV zqb[3], wpb[3];
@@ -276,8 +284,9 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
 #pragma unroll
             for (int k = 0; k < 3; k++) { zqb[k] = wb[k] + t1[k]; wpb[k] = wb[k] + t2[k]; }
         }
+        if constexpr (GQ)
 #pragma unroll
-        for (int k = 0; k < 3; k++) zb[k] = zb[k] + zqb[k] * qdi;
+            for (int k = 0; k < 3; k++) zb[k] = zb[k] + zqb[k] * qdi;
         gqdi = dot3(z, zqb);
         if (i > 0) {
             TV dxa[3], axd[3];
@@ -287,13 +296,13 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
 #pragma unroll
             for (int k = 0; k < 3; k++) {
                 dwb[k] += dxa[k];
-                db[k] = axd[k] + wp[k] * wa - ww * ab[k];
+                if constexpr (GQ) db[k] = axd[k] + wp[k] * wa - ww * ab[k];
                 wpb[k] = wpb[k] + ab[k] * wd + d[k] * wa - 2.0 * ad * wp[k];
-                ob[k] += db[k];
+                if constexpr (GQ) ob[k] += db[k];
             }
         }
         // ---- geometric adjoints -> q_i
-        {
+        if constexpr (GQ) {
             TV t1[3], t2[3], t3[3];
             cross3(t1, z, zb);
             cross3(t2, o, ob);
@@ -323,7 +332,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
             cross3(t2, wp, t2);
 #pragma unroll
             for (int k = 0; k < 3; k++) { a[k] = a[k] - t1[k] - t2[k]; o[k] = o[k] - d[k]; }
-            if constexpr (ADJ) {
+            if constexpr (ADJ && GQ) {
                 TV opxd[3];
                 cross3(opxd, o, db);
 #pragma unroll

@@ -147,7 +147,7 @@ template <int NJ, class TP> struct NodeIn {
 };
 // Per-lane results of node_fwd_rev, written straight to the node's global arrays: column v of
 // d tau / dw (Jt) and column v of grad^2 phi (raw, into W; k_eval_asm completes W in place).
-template <int NJ, int NF, int NV> struct NodeOut {
+template <int NJ, int NF, int NV, int CLS> struct NodeOut {
     double *Jt, *W;  // the node's blocks
     double *Ts;      // LDS: tau values of the node (direction-0 lane)
     int v;
@@ -162,11 +162,18 @@ template <int NJ, int NF, int NV> struct NodeOut {
         for (int a = 0; a < NF; a++)
             W[(2 * NJ + a) * NV + v] = fdir[3 * a] * dtan(gF[0]) + fdir[3 * a + 1] * dtan(gF[1]) + fdir[3 * a + 2] * dtan(gF[2]);
     }
+    // k_eval_asm reads the lower triangle (row >= column) of the Hessian: a qd lane (CLS 1) writes
+    // no q row (v >= NJ > i) and runs without the q-gradient adjoint (GQ = false); a q lane writes
+    // its whole column (the rows above the diagonal are never read)
     __device__ __forceinline__ void joint(int i, const Dual &t, const Dual &gq, const Dual &gqd) {
         Jt[i * NV + v] = t.d;
         if (v == 0) Ts[i] = t.v;
-        W[i * NV + v] = gq.d;
-        W[(NJ + i) * NV + v] = gqd.d;
+        if constexpr (CLS == 0) {
+            W[i * NV + v] = gq.d;
+            W[(NJ + i) * NV + v] = gqd.d;
+        } else {
+            if (NJ + i >= v) W[(NJ + i) * NV + v] = gqd.d;
+        }
     }
 };
 
@@ -209,7 +216,7 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     const double *q = A.q + b * S.q + (size_t)k * NJ;
     const double *qd = A.qd + b * S.u + (size_t)k * NJ;
     const double *Fv = A.F + b * S.f + (size_t)k * NFA;
-    NodeOut<NJ, NF, NV> out;
+    NodeOut<NJ, NF, NV, CLS> out;
     out.Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
     out.W = A.W + b * S.w + (size_t)k * NV * NV;
     out.Ts = Ts[g];
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
         node_fwd_rev<Dual, Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
     } else {
         NodeIn<NJ, double> in{qd, SCs[g], v};
-        node_fwd_rev<double, Dual, NJ>(M, F, fp, in, Fw, Cs[g], yl3, out);
+        node_fwd_rev<double, Dual, NJ, true, false>(M, F, fp, in, Fw, Cs[g], yl3, out);
         return;
     }
     // ---- q lanes: force columns of d tau / dw, line Jacobian column; node values (lane 0)
@@ -298,8 +305,9 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
 
 // Completes the condensed stage Hessian in place:
 //   H0_k = grad^2 L_k + J^T diag(2 wtau + Sigma_s) J + diag(Sigma_x) (+ cost curvature)
-// from the raw Hessian columns k_eval_node left in W (lower triangle read, both written) and the
-// Jacobian Jt; also the cost gradient gf.  One lane per (node, column v), NV lanes per node.
+// from the raw Hessian columns k_eval_node left in W and the Jacobian Jt; also the cost gradient
+// gf.  One lane per (node, column v), NV lanes per node.  W holds the lower triangle only (row u
+// >= column v), read and written in place; k_ipm_kkt mirrors it when it stages H0 in LDS.
 template <int NJ, int NF, int NL>
 __global__ __launch_bounds__(256) void k_eval_asm(OcpConst C, IpmArrays A, int batch) {
     constexpr int NV = 2 * NJ + NF;
@@ -332,7 +340,7 @@ __global__ __launch_bounds__(256) void k_eval_asm(OcpConst C, IpmArrays A, int b
                                                  A.tau_hi[(size_t)k * NJ + v]);
         }
 #pragma unroll
-        for (int u = 0; u < NV; u++) raw[u] = (u >= v) ? W[u * NV + v] : 0.0;
+        for (int u = 0; u < NV; u++) raw[u] = (u >= v && !(u >= 2 * NJ && v >= NJ)) ? W[u * NV + v] : 0.0;
     }
     __syncthreads();
     if (!run) return;
@@ -348,17 +356,17 @@ __global__ __launch_bounds__(256) void k_eval_asm(OcpConst C, IpmArrays A, int b
     }
     if (v >= NJ && v < 2 * NJ) diag += 2.0 * C.wqd;
     if (v >= 2 * NJ) diag += 2.0 * C.wF;
-    // phi is linear in F: the force-force block of the raw Hessian is zero (no lane computed it)
+    // phi is linear in F and d phi / dF does not depend on qd: the force rows of the qd and force
+    // columns of the raw Hessian are zero (no lane computed them; raw[] reads them as 0)
 #pragma unroll
     for (int u = 0; u < NV; u++) {
         if (u < v) continue;
         double gn = 0.0;
 #pragma unroll
         for (int j = 0; j < NJ; j++) gn += Wj[g][j] * Js[g][j][u] * Js[g][j][v];
-        double hh = ((u >= 2 * NJ && v >= 2 * NJ) ? 0.0 : raw[u]) + gn;
+        double hh = raw[u] + gn;
         if (u == v) hh += diag;
         W[u * NV + v] = hh;
-        W[v * NV + u] = hh;
     }
     const double *tv = A.tau + b * S.u + (size_t)k * NJ;
     double gfv = 0.0;
@@ -863,6 +871,13 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
     constexpr int NLA2 = NL > 0 ? NL : 1;
     constexpr int NVV = NV * NV;
     constexpr int NHR = (NVV + 63) / 64;     // H entries per lane
+    // H0 is stored as its lower triangle (k_eval_asm): lane entry e = (u, v) reads (max, min)
+    int hlo[NHR];
+#pragma unroll
+    for (int t = 0; t < NHR; t++) {
+        const int e = min(lane + 64 * t, NVV - 1), u = e / NV, v = e % NV;
+        hlo[t] = u >= v ? e : v * NV + u;
+    }
     constexpr int SLOT = MB * NJ + MB;       // Riccati slot (G_k | wv_k) doubles
     constexpr int NSR = (SLOT + 63) / 64;
     __shared__ double Hs[NVV];
@@ -980,7 +995,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
 #pragma unroll
         for (int t = 0; t < NHR; t++) {
             const int e = lane + 64 * t;
-            hr[t] = (e < NVV) ? W[(size_t)(N - 1) * NVV + e] : 0.0;
+            hr[t] = (e < NVV) ? W[(size_t)(N - 1) * NVV + hlo[t]] : 0.0;
         }
 #pragma unroll
         for (int t = 0; t < NJR; t++) {
@@ -1040,7 +1055,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
                 // unconditional loads from clamped addresses (a load whose value is selected
                 // against a constant is waited for on the spot)
 #pragma unroll
-                for (int t = 0; t < NHR; t++) hr[t] = W[(size_t)(k - 1) * NVV + min(lane + 64 * t, NVV - 1)];
+                for (int t = 0; t < NHR; t++) hr[t] = W[(size_t)(k - 1) * NVV + hlo[t]];
                 if constexpr (NL > 0) glr = Jl[(size_t)k * nl * n + min(lane, nl * n - 1)];
                 sgr = stg[(size_t)(k - 1) * SG + min(lane, SG - 1)];
                 if (dreg)
@@ -1606,7 +1621,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         bool ok0;
         merit(0.0, phi0, th0, ok0);
     }
-    // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx; lane e covers row v of node k's W
+    // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx; lane e covers row v of node k's W (lower triangle)
     double gdot = 0, pHp = (lane == 0) ? st.pcorr : 0.0;  // pcorr: whole-wave sum from k_ipm_kkt
     for (int e0 = lane; e0 < N * NV; e0 += 64 * 2) {
         double acc[2], gd[2];
@@ -1620,10 +1635,12 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
 #pragma unroll
             for (int a = 0; a < NF; a++) dx[2 * NJ + a] = dF[k * NFA + a];
             const double *Wr = W + (size_t)k * NV * NV + (size_t)v * NV;
+            // H0 is stored as its lower triangle: row v's part left of the diagonal counts twice
             double a = 0.0, dv = 0.0;
 #pragma unroll
             for (int w = 0; w < NV; w++) {
-                a += Wr[w] * dx[w];
+                const double hw = Wr[w];  // loaded unconditionally; the upper part is stale, never used
+                a += (w < v ? 2.0 * hw : (w == v ? hw : 0.0)) * dx[w];
                 if (w == v) dv = dx[w];
             }
             acc[u] = a * dv;

@@ -28,7 +28,7 @@ template <int NJ, class TP> struct In {
 
 template <int NJ> struct Out {
     Dual tau[NJ], gq[NJ], gqd[NJ];
-    double pfv[3], pfd[3], gFd[3];
+    double pfv[3], pfd[3], gFd[3] = {0.0, 0.0, 0.0};
     template <class TP> void frame(const TP *p) { for (int k = 0; k < 3; k++) { pfv[k] = val(p[k]); pfd[k] = dtan(p[k]); } }
     template <class TP> void force(const TP *g) { for (int k = 0; k < 3; k++) gFd[k] = dtan(g[k]); }
     void joint(int i, const Dual &t, const Dual &a, const Dual &b) { tau[i] = t; gq[i] = a; gqd[i] = b; }
@@ -51,8 +51,9 @@ static void run(const DevModel &M, const DevFrame &F, int fp, int nf, const doub
             In<NJ, Dual> in{q, qd, v};
             node_fwd_rev<Dual, Dual, NJ>(M, F, fp, in, Fw, c, yl3, o);
         } else {
+            // as k_eval_node's qd class: no q-gradient adjoint (GQ = false), no force row
             In<NJ, double> in{q, qd, v};
-            node_fwd_rev<double, Dual, NJ>(M, F, fp, in, Fw, c, yl3, o);
+            node_fwd_rev<double, Dual, NJ, true, false>(M, F, fp, in, Fw, c, yl3, o);
         }
         for (int j = 0; j < NJ; j++) Jt[j * nv + v] = o.tau[j].d;
         if (v < NJ) {
@@ -66,7 +67,8 @@ static void run(const DevModel &M, const DevFrame &F, int fp, int nf, const doub
             for (int k = 0; k < 3; k++) pf[k] = o.pfv[k];
         }
         for (int u = 0; u < NJ; u++) {
-            H[u * nv + v] = o.gq[u].d;
+            // q rows of a qd column: from the q lanes (already run) by symmetry
+            H[u * nv + v] = v < NJ ? o.gq[u].d : H[v * nv + u];
             H[(NJ + u) * nv + v] = o.gqd[u].d;
         }
         for (int a = 0; a < nf; a++) {
