@@ -879,14 +879,11 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
         hlo[t] = u >= v ? e : v * NV + u;
     }
     constexpr int SLOT = MB * NJ + MB;       // Riccati slot (G_k | wv_k) doubles
-    constexpr int NSR = (SLOT + 63) / 64;
     __shared__ double Hs[NVV];
     __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], Pn[NJ * NJ];
     __shared__ double Ks[NK * LDK], Rk[NK * NRK];
     __shared__ double Gl[NLA2 * NJ];
     __shared__ double Ss5[(NU > 2 ? NU - 2 : 1) * (NU > 2 ? NU - 2 : 1)];  // reduced Hessian (stage_ns.hpp)
-    __shared__ double xs[NJ], us[NU + NLA2], cs[NJ];
-    __shared__ double Sl[SLOT];
     __shared__ double Jl_s[NJ * NV];  // J_k (torque Jacobian) of the stage, regularised tries only
     // per-stage inputs of the recursion, computed for all stages at once by the whole wave (global
     // scratch, stage k contiguous): g_k (NV), c_k = q_k + h qd_k - q_{k+1} (NJ),
@@ -1209,111 +1206,101 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
     st.reg_last = reg;
 
     wave_mem_sync();  // the Riccati slots stored above are read back by other lanes below
-    // ---------------- forward sweep: du_k = Ku dx_k + ku, dyl_{k+1} = Kl dx_k + kl,
-    //                  dyc_k = P_{k+1} dx_{k+1} + p_{k+1} + Jl_{k+1}^T dyl_{k+1}
-    // (the node-(k+1) line constraint was pushed back onto stage k, so V_{k+1} does not contain
-    // it but the q_{k+1} row of the KKT does).  Slots and Jl_{k+1} are prefetched FD stages
-    // ahead into a register ring (a stage is shorter than one global-memory round trip).
-    constexpr int FD = 4;
-    constexpr int NGL = NL > 0 ? NL * NJ : 1;
-    double sr[FD][NSR], glr_f[FD], cr_f[FD];
-    // Every load is unconditional from a clamped address (lanes past the data read a valid
-    // element that is never used): a value selected between two loads, or between a load and a
-    // constant, makes the compiler wait for the load on the spot, which turned the ring into no
-    // prefetch at all.
-    auto fetch = [&](int kk, double *srr, double &g, double &cr) {
-        const double *Gn = G + (size_t)kk * MB * n, *wn = wv + (size_t)kk * MB;
+    // ---------------- forward sweep, serial part: dx_{k+1} = dx_k + h du_k + c_k with
+    //   (dqd_k, dF_k) = Ku dx_k + ku and dyl_{k+1} = Kl dx_k + kl (stage k's slot).  Lane a < NK
+    //   holds row a of [Ku ku; Kl kl] in registers, fetched FD stages ahead straight from global
+    //   memory, and dx_k is held uniformly by every lane (readlane broadcast of the six new
+    //   entries): a stage is one dot product, one update and the broadcast -- no LDS round trip.
+    //   dyc_k = P_{k+1} dx_{k+1} + p_{k+1} + Jl_{k+1}^T dyl_{k+1} does not feed the recursion and
+    //   is recovered afterwards for all stages at once.
+    // Every load is unconditional from a clamped address (a value selected between a load and a
+    // constant makes the compiler wait for the load on the spot, which would empty the ring).
+    constexpr int FD = 8;
+    const int ra = min(lane, NK - 1);  // slot row of this lane: qd 0..n-1, F, then the line multipliers
+    double rowr[FD][NJ], wkr[FD], ckr[FD];
+    auto fetch = [&](int kk, double *row, double &wk, double &ck) {
+        const double *src = G + (size_t)kk * MB * n + (size_t)ra * n;
+        if constexpr (NJ % 2 == 0) {
+            const double2 *s2 = reinterpret_cast<const double2 *>(src);  // 16-byte aligned: MB n, n even
 #pragma unroll
-        for (int t = 0; t < NSR; t++) {
-            const int e = lane + 64 * t;
-            const double *src = (e < MB * NJ) ? Gn + e : wn + min(e - MB * NJ, MB - 1);
-            srr[t] = *src;
+            for (int t = 0; t < NJ / 2; t++) {
+                const double2 v2 = s2[t];
+                row[2 * t] = v2.x;
+                row[2 * t + 1] = v2.y;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NJ; i++) row[i] = src[i];
         }
-        g = NL > 0 ? Jl[(size_t)min(kk + 1, N - 1) * NGL + min(lane, NGL - 1)] : 0.0;  // used only when con1
-        cr = stg[(size_t)kk * SG + NV + min(lane, NJ - 1)];             // c_k
-    };
-    // A stage's outputs (dq_k | dqd_k | dyc_k | dF_k | dyl_{k+1}) are staged in LDS and stored at
-    // the top of the next stage, before its fetch: the wait at a stage's top then only covers
-    // memory operations issued a stage earlier (vmcnt retires in order; stores issued at the end
-    // of a stage used to put a store round trip on every stage)
-    __shared__ double Fo[3 * NJ + NFA + NLA2];
-    auto flush = [&](int kk) {
-        if (kk == 0) {
-            if (lane < nf) dF[lane] = Fo[3 * n + lane];
-            if (lane < n) dyc[lane] = Fo[2 * n + lane];
-            return;
-        }
-        if (lane < n) {
-            dq[kk * n + lane] = Fo[lane];
-            dqd[kk * n + lane] = Fo[n + lane];
-            dyc[kk * n + lane] = Fo[2 * n + lane];
-        }
-        if (lane < nf) dF[kk * NFA + lane] = Fo[3 * n + lane];
-        if (kk + 1 < N && lane < nl) dyl[(kk + 1) * nl + lane] = Fo[3 * n + NFA + lane];
+        wk = wv[(size_t)kk * MB + ra];
+        ck = stg[(size_t)kk * SG + NV + min(lane, NJ - 1)];
     };
 #pragma unroll
-    for (int r = 0; r < FD; r++)
-        if (r < N) fetch(r, sr[r], glr_f[r], cr_f[r]);
-    for (int j = lane; j < n; j += 64) {
-        dq[j] = 0.0; dqd[j] = 0.0;
-        xs[j] = stg[NV + j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
-    }
+    for (int r = 0; r < FD; r++) fetch(min(r, N - 1), rowr[r], wkr[r], ckr[r]);
+    double xsv[NJ];  // dx_k, the same in every lane
+#pragma unroll
+    for (int j = 0; j < NJ; j++) xsv[j] = stg[NV + j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
+    for (int j = lane; j < n; j += 64) { dq[j] = 0.0; dqd[j] = 0.0; }
     for (int l = lane; l < nl; l += 64) { dyl[l] = 0.0; dyl[nl + l] = 0.0; }
     for (int k0 = 0; k0 < N; k0 += FD) {
 #pragma unroll
         for (int r = 0; r < FD; r++) {
             const int k = k0 + r;
             if (k >= N) break;
-            // slot k -> LDS; prefetch slot k + FD into the freed ring entry
+            double row[NJ], wk = wkr[r], ck = ckr[r];
 #pragma unroll
-            for (int t = 0; t < NSR; t++) {
-                const int e = lane + 64 * t;
-                if (e < SLOT) Sl[e] = sr[r][t];
-            }
-            if (lane < NGL) Gl[lane] = glr_f[r];
-            if (lane < NJ) Stg[lane] = cr_f[r];
-            if (k > 0) flush(k - 1);
-            fetch(min(k + FD, N - 1), sr[r], glr_f[r], cr_f[r]);  // past the end: slot N-1 again, unused
-            wave_lds_sync();
-            const double *Gk = Sl, *wk = Sl + MB * NJ;
-            if (k == 0) {
-                for (int a = lane; a < nf; a += 64) Fo[3 * n + a] = wk[NJ + a];  // dF_0
-                for (int j = lane; j < n; j += 64) {  // dyc_0 = P_1 dx_1 + p_1 (stage-1 line is masked)
-                    double a = wk[NU + NL + j];
-                    for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * xs[i];
-                    Fo[2 * n + j] = a;
-                }
-                wave_lds_sync();
+            for (int i = 0; i < NJ; i++) row[i] = rowr[r][i];
+            fetch(min(k + FD, N - 1), rowr[r], wkr[r], ckr[r]);  // past the end: slot N-1 again, unused
+            if (k == 0) {  // only dF_0 is free; it sits in the ku slot of stage 0
+                if (lane >= NJ && lane < NU) dF[lane - NJ] = wk;
                 continue;
             }
-            for (int a = lane; a < NK; a += 64) {
-                double v = wk[a];
-                for (int i = 0; i < n; i++) v += Gk[a * n + i] * xs[i];
-                us[a] = v;
-            }
-            for (int j = lane; j < n; j += 64) Fo[j] = xs[j];  // dq_k
-            wave_lds_sync();
-            for (int j = lane; j < n; j += 64) {
-                Fo[n + j] = us[j];  // dqd_k
-                cs[j] = xs[j] + h * us[j] + Stg[j];
-            }
-            for (int a = lane; a < nf; a += 64) Fo[3 * n + a] = us[NJ + a];  // dF_k
+            double us = wk;
+#pragma unroll
+            for (int i = 0; i < NJ; i++) us += row[i] * xsv[i];
             const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
-            for (int l = lane; l < nl; l += 64) Fo[3 * n + NFA + l] = con1 ? us[NU + l] : 0.0;  // dyl_{k+1}
-            wave_lds_sync();
-            for (int j = lane; j < n; j += 64) {
-                double a = wk[NU + NL + j];
-                for (int i = 0; i < n; i++) a += Gk[(NU + NL) * n + j * n + i] * cs[i];
-                if (con1)
-                    for (int l = 0; l < nl; l++) a += Gl[l * n + j] * us[NU + l];
-                Fo[2 * n + j] = a;  // dyc_k
-                xs[j] = cs[j];
+            double xj = xsv[0];
+#pragma unroll
+            for (int j = 1; j < NJ; j++) xj = (lane == j) ? xsv[j] : xj;
+            const double cs = xj + h * us + ck;  // dx_{k+1}, entry `lane` (lanes < n)
+            if (lane < n) {
+                dq[k * n + lane] = xj;
+                dqd[k * n + lane] = us;
+            } else if (lane < NU) {
+                dF[k * NFA + lane - NJ] = us;
+            } else if (lane < NK) {
+                if (k + 1 < N) dyl[(k + 1) * nl + lane - NU] = con1 ? us : 0.0;
             }
-            wave_lds_sync();
+#pragma unroll
+            for (int j = 0; j < NJ; j++) xsv[j] = readlane_d(cs, j);
         }
     }
-    flush(N - 1);
-    for (int j = lane; j < n; j += 64) dq[N * n + j] = xs[j];
+    for (int j = lane; j < n; j += 64) dq[N * n + j] = xsv[j];
+    wave_mem_sync();  // dq_{k+1}, dyl_{k+1} are read back by other lanes
+    // ---------------- forward sweep, parallel part: dyc_k for every stage
+    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        double a[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + 64 * u, N * n - 1);
+            const int k = e / n, j = e % n;
+            const double *Pj = G + (size_t)k * MB * n + (size_t)(NU + NL + j) * n;
+            double v = wv[(size_t)k * MB + NU + NL + j];
+#pragma unroll
+            for (int i = 0; i < NJ; i++) v += Pj[i] * dq[(k + 1) * n + i];
+            const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
+            const int k1 = min(k + 1, N - 1);
+#pragma unroll
+            for (int l = 0; l < NL; l++) {
+                const double jl = Jl[((size_t)k1 * nl + l) * n + j], yl1 = dyl[k1 * nl + l];
+                if (con1) v += jl * yl1;  // (contracted like the sweep's own update: same round-off)
+            }
+            a[u] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++)
+            if (e0 + 64 * u < N * n) dyc[e0 + 64 * u] = a[u];
+    }
     __threadfence_block();
     __syncthreads();
 
