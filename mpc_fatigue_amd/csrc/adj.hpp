@@ -82,20 +82,25 @@ template <class T> MF_HD void rodrigues_rows(T *R, const T *A, const double *ax,
 // frame-point adjoints, Gamma, Obar) feed d phi / dq alone.  A lane of a qd direction whose
 // caller needs only the qd rows of its Hessian column (the q rows follow from the q lanes by
 // symmetry; the force row is identically zero: d phi / dF does not depend on qd) runs GQ = false.
-template <class TP, class TV, int NJ, bool ADJ = true, bool GQ = true, class In, class Emit>
-MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &in, const double *Fw, const double *c,
-                        const double *yl, Emit &em) {
-    TP R[9], o[3], Lz[3], Loz[3];
-    TV w[3], dw[3], a[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        w[k] = TV(0.0); dw[k] = TV(0.0); a[k] = TV(-M.g[k]);
-        Lz[k] = TP(0.0); Loz[k] = TP(0.0);
-    }
+template <class TP, class TV> struct SweepState {
+    TP R[9], o[3], Lz[3], Loz[3];                                  // pose, c-weighted axis prefix sums
+    TV w[3], dw[3], a[3];                                          // twist, acceleration
+    TV Mt[3], Ft[3], wb[3], dwb[3], ab[3], G[3], Ob[3];            // reverse sweep
+};
 
-    // ---------------- forward sweep: pose, twist, acceleration; prefix Lambda
+// TV value of an input that may carry a tangent (a plain-double sweep takes its value)
+template <class TV, class T> MF_HD TV as_tv(const T &x) {
+    if constexpr (sizeof(TV) == sizeof(double)) return val(x);
+    else return TV(x);
+}
+
+// forward sweep over joints i0 .. i1-1: pose, twist, acceleration; prefix Lambda
+template <class TP, class TV, int NJ, bool ADJ, class In>
+MF_HD void fwd_range(const DevModel &M, int i0, int i1, const In &in, const double *c, SweepState<TP, TV> &S) {
+    TP(&R)[9] = S.R; TP(&o)[3] = S.o; TP(&Lz)[3] = S.Lz; TP(&Loz)[3] = S.Loz;
+    TV(&w)[3] = S.w; TV(&dw)[3] = S.dw; TV(&a)[3] = S.a;
 #pragma unroll 1
-    for (int i = 0; i < NJ; i++) {
+    for (int i = i0; i < i1; i++) {
         const DevJoint &J = M.j[i];
         TP A[9], on[3], z[3];
         if (i == 0) {
@@ -123,7 +128,7 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
         in.sincos(i, s, cq);
         rodrigues_rows(R, A, J.axis, s, TP(1.0) - cq);
         TV zq[3], t[3];
-        const TV qdi = in.qd(i);
+        const TV qdi = as_tv<TV>(in.qd(i));
 #pragma unroll
         for (int k = 0; k < 3; k++) zq[k] = z[k] * qdi;
         cross3(t, w, zq);
@@ -136,19 +141,22 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
             for (int k = 0; k < 3; k++) { Lz[k] += z[k] * c[i]; Loz[k] += oz[k] * c[i]; }
         }
     }
+}
 
-    // ---------------- reverse sweep
-    TV Mt[3], Ft[3], wb[3], dwb[3], ab[3], G[3], Ob[3];
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        Mt[k] = TV(0.0); Ft[k] = TV(0.0); wb[k] = TV(0.0); dwb[k] = TV(0.0);
-        ab[k] = TV(0.0); G[k] = TV(0.0); Ob[k] = TV(0.0);
-    }
+// reverse sweep over joints i_hi .. i_lo (descending); the state holds joint i_hi's forward
+// quantities on entry and joint i_lo - 1's on exit
+template <class TP, class TV, int NJ, bool ADJ, bool GQ, class In, class Emit>
+MF_HD void rev_range(const DevModel &M, const DevFrame &F, int fp, int i_hi, int i_lo, const In &in, const double *Fw,
+                     const double *c, const double *yl, Emit &em, SweepState<TP, TV> &S) {
+    TP(&R)[9] = S.R; TP(&o)[3] = S.o; TP(&Lz)[3] = S.Lz; TP(&Loz)[3] = S.Loz;
+    TV(&w)[3] = S.w; TV(&dw)[3] = S.dw; TV(&a)[3] = S.a;
+    TV(&Mt)[3] = S.Mt; TV(&Ft)[3] = S.Ft; TV(&wb)[3] = S.wb; TV(&dwb)[3] = S.dwb; TV(&ab)[3] = S.ab;
+    TV(&G)[3] = S.G; TV(&Ob)[3] = S.Ob;
 #pragma unroll 1
-    for (int i = NJ - 1; i >= 0; i--) {
+    for (int i = i_hi; i >= i_lo; i--) {
         const DevJoint &J = M.j[i];
         const double m = J.m;
-        const TV qdi = in.qd(i);
+        const TV qdi = as_tv<TV>(in.qd(i));
         TP z[3];
         matc_vec(z, R, J.axis);  // z_i = A_i axis = R_i axis (E_i leaves the axis fixed)
         TV zq[3], wp[3], dwp[3];
@@ -351,6 +359,68 @@ MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &
                 for (int cc = 0; cc < 3; cc++)
                     R[3 * rr + cc] = A[3 * rr] * J.RX[3 * cc] + A[3 * rr + 1] * J.RX[3 * cc + 1] + A[3 * rr + 2] * J.RX[3 * cc + 2];
         }
+    }
+}
+
+template <class TP, class TV> MF_HD void sweep_init(const DevModel &M, SweepState<TP, TV> &S) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        S.w[k] = TV(0.0); S.dw[k] = TV(0.0); S.a[k] = TV(-M.g[k]);
+        S.Lz[k] = TP(0.0); S.Loz[k] = TP(0.0);
+        S.Mt[k] = TV(0.0); S.Ft[k] = TV(0.0); S.wb[k] = TV(0.0); S.dwb[k] = TV(0.0);
+        S.ab[k] = TV(0.0); S.G[k] = TV(0.0); S.Ob[k] = TV(0.0);
+    }
+}
+
+
+template <class TP, class TV, int NJ, bool ADJ = true, bool GQ = true, class In, class Emit>
+MF_HD void node_fwd_rev(const DevModel &M, const DevFrame &F, int fp, const In &in, const double *Fw, const double *c,
+                        const double *yl, Emit &em) {
+    SweepState<TP, TV> S;
+    sweep_init(M, S);
+    fwd_range<TP, TV, NJ, ADJ>(M, 0, NJ, in, c, S);
+    rev_range<TP, TV, NJ, ADJ, GQ>(M, F, fp, NJ - 1, 0, in, Fw, c, yl, em, S);
+}
+
+// The sweep of a q direction v, split where its tangents vanish.  Every pose and velocity
+// quantity of joints i < v is a function of q_0..q_i and qd_0..qd_i only, so its q_v tangent is
+// identically zero: the forward sweep runs plain FP64 over joints 0..v-1 and switches to Dual at
+// joint v (whose angle carries the tangent); the reverse sweep runs Dual over joints NJ-1..v and
+// then, with the pose tangents dropped (exactly zero), over joints v-1..0 as a qd-class sweep
+// (TP = double, TV = Dual: the adjoints' tangents are not zero) without the q-gradient (GQ = false:
+// its rows i < v are the Hessian's upper triangle, which no caller reads).  em.force is not called
+// when the frame parent is below v (that Hessian entry is exactly zero then).  The caller's In
+// functor provides sincos / qd for both scalar types (template members).
+template <int NJ, class In, class Emit>
+MF_HD void node_fwd_rev_split(const DevModel &M, const DevFrame &F, int fp, int v, const In &in, const double *Fw,
+                              const double *c, const double *yl, Emit &em) {
+    SweepState<double, double> S0;
+    sweep_init(M, S0);
+    fwd_range<double, double, NJ, true>(M, 0, v, in, c, S0);
+    SweepState<Dual, Dual> S1;
+#pragma unroll
+    for (int k = 0; k < 9; k++) S1.R[k] = Dual(S0.R[k]);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        S1.o[k] = Dual(S0.o[k]); S1.Lz[k] = Dual(S0.Lz[k]); S1.Loz[k] = Dual(S0.Loz[k]);
+        S1.w[k] = Dual(S0.w[k]); S1.dw[k] = Dual(S0.dw[k]); S1.a[k] = Dual(S0.a[k]);
+        S1.Mt[k] = Dual(0.0); S1.Ft[k] = Dual(0.0); S1.wb[k] = Dual(0.0); S1.dwb[k] = Dual(0.0);
+        S1.ab[k] = Dual(0.0); S1.G[k] = Dual(0.0); S1.Ob[k] = Dual(0.0);
+    }
+    fwd_range<Dual, Dual, NJ, true>(M, v, NJ, in, c, S1);
+    rev_range<Dual, Dual, NJ, true, true>(M, F, fp, NJ - 1, v, in, Fw, c, yl, em, S1);
+    if (v > 0) {
+        SweepState<double, Dual> S2;
+#pragma unroll
+        for (int k = 0; k < 9; k++) S2.R[k] = S1.R[k].v;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            S2.o[k] = S1.o[k].v; S2.Lz[k] = S1.Lz[k].v; S2.Loz[k] = S1.Loz[k].v;
+            S2.w[k] = S1.w[k]; S2.dw[k] = S1.dw[k]; S2.a[k] = S1.a[k];
+            S2.Mt[k] = S1.Mt[k]; S2.Ft[k] = S1.Ft[k]; S2.wb[k] = S1.wb[k]; S2.dwb[k] = S1.dwb[k];
+            S2.ab[k] = S1.ab[k]; S2.G[k] = S1.G[k]; S2.Ob[k] = S1.Ob[k];
+        }
+        rev_range<double, Dual, NJ, true, false>(M, F, fp, v - 1, 0, in, Fw, c, yl, em, S2);
     }
 }
 

@@ -303,6 +303,159 @@ __global__ __launch_bounds__(256) void k_eval_node(const DevModel *__restrict__ 
     }
 }
 
+// ---- q directions: one wavefront = one direction v x 64 nodes (k_eval_q)
+// A wave whose lanes all carry the tangent of the same angle q_v runs node_fwd_rev_split: plain FP64
+// over the joints below v in the forward sweep and, in the reverse sweep, the qd-class arithmetic
+// (plain pose, no q-gradient) over those joints -- the tangents it drops are exactly zero.  Block
+// (node group, v) = blockIdx (grp * NJ + v): the NJ directions of a node group are adjacent.  Each
+// lane writes column v of d tau / dw, the lower part (rows >= v) of column v of the raw Hessian, the
+// force column entry of row v, the line-Jacobian column v and (v = 0) the node's tau, cost and line
+// residual.
+struct QIn {
+    const double (*sc)[2];  // LDS: sin / cos of the lane's joint angles
+    const double *xqd;      // LDS: the lane's joint velocities
+    int v;
+    __device__ __forceinline__ Dual qd(int i) const { return Dual(xqd[i], 0.0); }
+    __device__ __forceinline__ void sincos(int i, double &s, double &c) const { s = sc[i][0]; c = sc[i][1]; }
+    __device__ __forceinline__ void sincos(int i, Dual &s, Dual &c) const {
+        const double sv = sc[i][0], cv = sc[i][1], t = (v == i) ? 1.0 : 0.0;
+        s = Dual(sv, cv * t);
+        c = Dual(cv, -sv * t);
+    }
+};
+template <int NJ, int NF, int NV> struct QOut {
+    double *Jt, *W;
+    double *Ts;  // LDS: tau values of the lane's node
+    int v;
+    bool forced;
+    const double *fdir;
+    double pfv[3], pfd[3];
+    template <class TP> __device__ __forceinline__ void frame(const TP *p) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) { pfv[k] = val(p[k]); pfd[k] = dtan(p[k]); }
+    }
+    template <class TP> __device__ __forceinline__ void force(const TP *gF) {
+        forced = true;
+#pragma unroll
+        for (int a = 0; a < NF; a++)
+            W[(2 * NJ + a) * NV + v] = fdir[3 * a] * dtan(gF[0]) + fdir[3 * a + 1] * dtan(gF[1]) + fdir[3 * a + 2] * dtan(gF[2]);
+    }
+    __device__ __forceinline__ void joint(int i, const Dual &t, const Dual &gq, const Dual &gqd) {
+        Jt[i * NV + v] = t.d;
+        Ts[i] = t.v;
+        if (i >= v) W[i * NV + v] = gq.d;
+        W[(NJ + i) * NV + v] = gqd.d;
+    }
+};
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(64) void k_eval_q(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                               OcpConst C, IpmArrays A, int batch) {
+    constexpr int NV = 2 * NJ + NF;
+    constexpr int NFA = NF > 0 ? NF : 1;
+    __shared__ ModelLds<NJ> Ml;
+    const DevModel &M = Ml.get();
+    __shared__ DevFrame F;
+    __shared__ double SCs[64][NJ][2], QDs[64][NJ], Cs[64][NJ], Ts[64][NJ];
+    const int v = (int)(blockIdx.x % NJ);
+    const long grp = blockIdx.x / NJ;
+    const int lane = threadIdx.x;
+    const int N = C.N;
+    const long nslots = (long)*A.nrun * N;  // nodes of the compacted running set
+    if (grp * 64 >= nslots) return;         // block past the running set (uniform)
+    Ml.load(Mg);
+    stage_lds(&F, Fg);
+    const long node = grp * 64 + lane;
+    bool run = node < nslots;
+    int b = 0, k = 0;
+    if (run) {
+        b = A.list[node / N];
+        k = (int)(node % N);
+        run = A.st[b].status == ST_RUNNING;
+    }
+    const IpmSizes S = ipm_sizes(C);
+    const double *q = A.q + b * S.q + (size_t)k * NJ;
+    const double *qd = A.qd + b * S.u + (size_t)k * NJ;
+    const double *Fv = A.F + b * S.f + (size_t)k * NFA;
+    double Fw[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < NF; a++) acc += Fv[a] * C.fdir[3 * a + r];
+        Fw[r] = acc;
+    }
+    const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
+    if (run) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            sincos(q[j], &SCs[lane][j][0], &SCs[lane][j][1]);
+            QDs[lane][j] = qd[j];
+        }
+        // torque weights c = y_tau + 2 wtau tau (tau at the iterate first when wtau != 0)
+        const double *yd = A.yd + b * S.u + (size_t)k * NJ;
+        if (C.wtau != 0.0) {
+            struct WOut {
+                double *c;
+                const double *yd;
+                double w2;
+                __device__ void frame(const double *) {}
+                __device__ void force(const double *) {}
+                __device__ void joint(int j, double t, double, double) { c[j] = yd[j] + w2 * t; }
+            } wo{Cs[lane], yd, 2.0 * C.wtau};
+            ArrIn<NJ> in0{q, qd};
+            node_values<NJ>(M, F, fp, in0, Fw, wo);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NJ; j++) Cs[lane][j] = yd[j];
+        }
+    }
+    __syncthreads();
+    if (!run) return;
+    double yl3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int l = 0; l < NL; l++) yl3[l] = A.yl[b * S.l + (size_t)k * NL + l];
+    QOut<NJ, NF, NV> out;
+    out.Jt = A.Jt + b * S.jt + (size_t)k * NJ * NV;
+    out.W = A.W + b * S.w + (size_t)k * NV * NV;
+    out.Ts = Ts[lane];
+    out.v = v;
+    out.forced = false;
+    out.fdir = C.fdir;
+    QIn in{SCs[lane], QDs[lane], v};
+    node_fwd_rev_split<NJ>(M, F, fp, v, in, Fw, Cs[lane], yl3, out);
+    if (!out.forced)  // frame parent below v: the force row of column v is exactly zero
+#pragma unroll
+        for (int a = 0; a < NF; a++) out.W[(2 * NJ + a) * NV + v] = 0.0;
+    // force columns of d tau / dw (row v), line Jacobian column v; node values (v = 0)
+#pragma unroll
+    for (int a = 0; a < NF; a++)
+        out.Jt[v * NV + 2 * NJ + a] = -(C.fdir[3 * a] * out.pfd[0] + C.fdir[3 * a + 1] * out.pfd[1] +
+                                        C.fdir[3 * a + 2] * out.pfd[2]);
+    if (NL > 0) {
+        double *Jl = A.Jl + b * S.jl + (size_t)k * NL * NJ;
+#pragma unroll
+        for (int l = 0; l < NL; l++) Jl[l * NJ + v] = out.pfd[l];
+    }
+    if (v == 0) {
+        double *tvo = A.tau + b * S.u + (size_t)k * NJ;
+        double c = 0.0;
+#pragma unroll
+        for (int a = 0; a < NF; a++) c += C.wF * Fv[a] * Fv[a];
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            const double tj = Ts[lane][j];
+            tvo[j] = tj;
+            c += C.wqd * QDs[lane][j] * QDs[lane][j] + C.wtau * tj * tj;
+        }
+        A.cost[b * S.cost + k] = c;
+        if (NL > 0) {
+            double *lv = A.line + b * S.l + (size_t)k * NL;
+#pragma unroll
+            for (int l = 0; l < NL; l++) lv[l] = out.pfv[l] - A.lref[b * 2 + l];
+        }
+    }
+}
+
 // Completes the condensed stage Hessian in place:
 //   H0_k = grad^2 L_k + J^T diag(2 wtau + Sigma_s) J + diag(Sigma_x) (+ cost curvature)
 // from the raw Hessian columns k_eval_node left in W and the Jacobian Jt; also the cost gradient
@@ -1840,7 +1993,8 @@ struct IpmLaunch {
         long nodes = (long)nact * C.N;
         if (phase == 0) {
             const int nb = (int)((nodes + NPB - 1) / NPB);
-            hipLaunchKernelGGL((k_eval_node<NJ, NF, NL, 0>), dim3(nb), dim3(256), 0, s, M, F, C, A, batch, nb);
+            hipLaunchKernelGGL((k_eval_q<NJ, NF, NL>), dim3((unsigned)(((nodes + 63) / 64) * NJ)), dim3(64), 0, s, M, F, C,
+                               A, batch);
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL, 1>), dim3(nb), dim3(256), 0, s, M, F, C, A, batch, nb);
         } else if (phase == 1) {
             hipLaunchKernelGGL((k_eval_asm<NJ, NF, NL>), dim3((unsigned)((nodes + NPBA - 1) / NPBA)), dim3(256), 0, s,

@@ -26,6 +26,18 @@ template <int NJ, class TP> struct In {
     }
 };
 
+// inputs for the split q-direction sweep (node_fwd_rev_split): sincos / qd for both scalar types
+template <int NJ> struct InSplit {
+    const double *xq, *xqd;
+    int v;
+    Dual qd(int i) const { return Dual(xqd[i], 0.0); }
+    void sincos(int i, double &s, double &c) const { sincos_t(xq[i], s, c); }
+    void sincos(int i, Dual &s, Dual &c) const { sincos_t(Dual(xq[i], v == i ? 1.0 : 0.0), s, c); }
+};
+
+static int g_split = 0;  // 1: the q directions run node_fwd_rev_split, as k_eval_node's q class does
+extern "C" void adj_set_split(int on) { g_split = on; }
+
 template <int NJ> struct Out {
     Dual tau[NJ], gq[NJ], gqd[NJ];
     double pfv[3], pfd[3], gFd[3] = {0.0, 0.0, 0.0};
@@ -47,7 +59,10 @@ static void run(const DevModel &M, const DevFrame &F, int fp, int nf, const doub
     }
     for (int v = 0; v < 2 * NJ; v++) {
         Out<NJ> o;
-        if (v < NJ) {
+        if (v < NJ && g_split) {
+            InSplit<NJ> in{q, qd, v};
+            node_fwd_rev_split<NJ>(M, F, fp, v, in, Fw, c, yl3, o);
+        } else if (v < NJ) {
             In<NJ, Dual> in{q, qd, v};
             node_fwd_rev<Dual, Dual, NJ>(M, F, fp, in, Fw, c, yl3, o);
         } else {
@@ -68,7 +83,8 @@ static void run(const DevModel &M, const DevFrame &F, int fp, int nf, const doub
         }
         for (int u = 0; u < NJ; u++) {
             // q rows of a qd column: from the q lanes (already run) by symmetry
-            H[u * nv + v] = v < NJ ? o.gq[u].d : H[v * nv + u];
+            // (the split sweep computes no q rows above the diagonal: those follow by symmetry too)
+            H[u * nv + v] = (v < NJ && !(g_split && u < v)) ? o.gq[u].d : H[v * nv + u];
             H[(NJ + u) * nv + v] = o.gqd[u].d;
         }
         for (int a = 0; a < nf; a++) {

@@ -51,8 +51,11 @@ CASES = [("pilz_robot_6DOF.urdf", "prbt_link_5", 1), ("pilz_robot_6DOF.urdf", "p
          ("pilz_robot_6DOF_second.urdf", "end_effector", 2)]
 
 
+@pytest.mark.parametrize("split", [0, 1])
 @pytest.mark.parametrize("urdf,frame,nf", CASES)
-def test_fwd_rev_matches_hyperdual_oracle(adj, urdf, frame, nf):
+def test_fwd_rev_matches_hyperdual_oracle(adj, urdf, frame, nf, split):
+    """split = 1: the q directions run node_fwd_rev_split (plain FP64 below joint v, k_eval_node's q class)."""
+    adj.adj_set_split(split)
     xml = open(PR.urdf_path(urdf)).read()
     m = load_urdf_file(PR.urdf_path(urdf))
     n = m.nq
