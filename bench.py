@@ -94,7 +94,7 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="horizons in the CPU sample (0: 4 per thread)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU runs (median reported)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1024-shard and single-problem figures")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=4,
                     help="independent steps in flight (own workspace, stream and host thread each)")
     args = ap.parse_args()
 

@@ -73,6 +73,14 @@ __device__ __forceinline__ void wave_argmax(double &v, int &idx) {
 // s_waitcnt lgkmcnt(0) plus a compiler memory barrier.  __syncthreads() is a workgroup
 // release fence and also waits for vmcnt(0) while global stores are outstanding -- and vmcnt
 // retires in order, so it would drain every register prefetch in flight as well.
+// The lane index as a value the compiler cannot prove loop-invariant: index arithmetic derived
+// from it is recomputed where it is used instead of being hoisted out of the serial stage loops
+// and held in registers across them (occupancy of the Riccati kernels).
+__device__ __forceinline__ int lane_opaque() {
+    int l = threadIdx.x;
+    __asm__ volatile("" : "+v"(l));
+    return l;
+}
 __device__ __forceinline__ void wave_lds_sync() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // all of the wave's memory operations (global stores read back by other lanes, LDS) complete
 __device__ __forceinline__ void wave_mem_sync() { __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
@@ -84,7 +92,7 @@ struct BKInertia {
 // perm/piv: LDS int arrays of length >= m.
 template <int LD>
 __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
-    const int lane = threadIdx.x;
+    const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     BKInertia in{0, 0, 0};
     for (int i = lane; i < m; i += 64) perm[i] = i;
@@ -192,7 +200,7 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
 // LDS reads issue back to back instead of one dependent round trip per candidate.
 template <int LD, int M>
 __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
-    const int lane = threadIdx.x;
+    const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     BKInertia in{0, 0, 0};
     if (lane < M) perm[lane] = lane;
@@ -324,7 +332,7 @@ template <int LD, int NR, int MU, int ML>
 __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in) {
     constexpr int M = MU + ML;
     static_assert(ML <= 2, "Schur block of at most 2 rows");
-    const int lane = threadIdx.x;
+    const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     double a[M], y[NR];
 #pragma unroll
@@ -424,7 +432,7 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
 // acts on rows >= t + 1, or >= t + 2 when t opens a 2x2 pivot (its partner row belongs to D).
 template <int LD, int NR, int M>
 __device__ void bk_solve_cols(const double *A, const int *perm, const int *piv, double *B, int nr) {
-    const int c = threadIdx.x;
+    const int c = lane_opaque();
     double y[M];
     int pv[M];
     if (c < nr) {
@@ -474,7 +482,7 @@ __device__ void bk_solve_cols(const double *A, const int *perm, const int *piv, 
 // Y: LDS scratch m x NR.
 template <int LD, int NR>
 __device__ void bk_solve_wave(const double *A, int m, const int *perm, const int *piv, double *B, int nr, double *Y) {
-    const int lane = threadIdx.x;
+    const int lane = lane_opaque();
     for (int e = lane; e < m * nr; e += 64) {
         int i = e / nr, c = e % nr;
         Y[i * NR + c] = B[perm[i] * NR + c];

@@ -937,7 +937,7 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
 }
 
 template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+__global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
     constexpr int n = NJ, nf = NF, nl = NL;
     constexpr int NV = 2 * NJ + NF;
@@ -1159,6 +1159,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
         auto brow = [&](int c) { return c < NU ? (c < NJ ? NF + c : c - NJ) : c; };
         wave_lds_sync();
         for (int k = N - 1; k >= 0; k--) {
+            const int lane = lane_opaque();  // per-stage index arithmetic stays inside the stage
             // ---- H_k = H0_k (+ regularisation) into LDS; prefetch H0_{k-1}, Jl_k (, J_{k-1})
             STAMP(18);
             if (lane < SG) Stg[lane] = sgr;
@@ -1368,7 +1369,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_kkt(const DevModel *__restrict__ 
     //   is recovered afterwards for all stages at once.
     // Every load is unconditional from a clamped address (a value selected between a load and a
     // constant makes the compiler wait for the load on the spot, which would empty the ring).
-    constexpr int FD = 8;
+    constexpr int FD = 4;
     const int ra = min(lane, NK - 1);  // slot row of this lane: qd 0..n-1, F, then the line multipliers
     double rowr[FD][NJ], wkr[FD], ckr[FD];
     auto fetch = [&](int kk, double *row, double &wk, double &ck) {

@@ -33,7 +33,7 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
                                                const double *gsk, const double *elk, double h, double *Ss5,
                                                double *Rk) {
     constexpr int NU = NJ + NF, NR = NU - 2;
-    const int lane = threadIdx.x;
+    const int lane = lane_opaque();
     const double hh = h * h;
     // Q entry (controls x, y; x, y < NJ are joint velocities)
     auto Qe = [&](int x, int y) {
@@ -132,14 +132,15 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
         const double bJ0 = bu(J0), bJ1 = bu(J1);
         const double rJ0 = bJ0 - q00 * up0 - q01 * up1;
         const double rJ1 = bJ1 - q01 * up0 - q11 * up1;
-        double y[NR], z0[NR], z1[NR], qJ0R[NR], qJ1R[NR];
+        // Z_JR and Q_JR are re-read from LDS after the triangular solves rather than held through
+        // them (register budget of the whole Riccati kernel)
+        double y[NR];
 #pragma unroll
         for (int m = 0; m < NR; m++) {
             const int x = Ridx(m);
-            Zc(m, z0[m], z1[m]);
-            qJ0R[m] = Qe(J0, x);
-            qJ1R[m] = Qe(J1, x);
-            y[m] = bu(x) - qJ0R[m] * up0 - qJ1R[m] * up1 + z0[m] * rJ0 + z1[m] * rJ1;
+            double z0, z1;
+            Zc(m, z0, z1);
+            y[m] = bu(x) - Qe(J0, x) * up0 - Qe(J1, x) * up1 + z0 * rJ0 + z1 * rJ1;
         }
 #pragma unroll
         for (int i = 0; i < NR; i++)
@@ -151,12 +152,18 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
         for (int i = NR - 1; i >= 0; i--)
 #pragma unroll
             for (int k = i + 1; k < NR; k++) y[i] -= L[k][i] * y[k];
-        double uJ0 = up0, uJ1 = up1;
+        double uJ0 = up0, uJ1 = up1, sJ0 = 0.0, sJ1 = 0.0;
 #pragma unroll
-        for (int m = 0; m < NR; m++) { uJ0 += z0[m] * y[m]; uJ1 += z1[m] * y[m]; }
-        double t0 = bJ0 - q00 * uJ0 - q01 * uJ1, t1 = bJ1 - q01 * uJ0 - q11 * uJ1;
-#pragma unroll
-        for (int m = 0; m < NR; m++) { t0 -= qJ0R[m] * y[m]; t1 -= qJ1R[m] * y[m]; }
+        for (int m = 0; m < NR; m++) {
+            const int x = Ridx(m);
+            double z0, z1;
+            Zc(m, z0, z1);
+            uJ0 += z0 * y[m];
+            uJ1 += z1 * y[m];
+            sJ0 += Qe(J0, x) * y[m];
+            sJ1 += Qe(J1, x) * y[m];
+        }
+        const double t0 = bJ0 - q00 * uJ0 - q01 * uJ1 - sJ0, t1 = bJ1 - q01 * uJ0 - q11 * uJ1 - sJ1;
         // D_J^T l = t  ->  l = D_J^{-T} t
         const double l0 = i00 * t0 + i10 * t1, l1 = i01 * t0 + i11 * t1;
 #pragma unroll
