@@ -9,7 +9,12 @@ namespace mf {
 // Per-problem scalar state of the interior-point iteration.
 struct ProbState {
     double mu, nu, reg_last, E0, cviol, obj;
-    double tau_fb, pcorr;  // fraction to the boundary, step-curvature correction (k_ipm_kkt -> k_ipm_post)
+    double tau_fb;         // fraction to the boundary parameter (k_ipm_pre -> k_kkt_recover)
+    double kkt_dw, kkt_dc; // regularisation of the accepted factorisation (k_ipm_kkt -> k_kkt_recover)
+    // step quantities for the line search (k_kkt_recover -> k_ipm_post): primal / dual step bounds
+    // (fraction to the boundary), grad(phi)^T dx and dx^T (W + Sigma) dx
+    double ap, az, gdot, pHp;
+    double alpha;          // accepted primal step (k_ipm_post -> k_post_update)
     int reg_tier;     // inertia correction of the last iteration: 0 none, 1 force block, 2 all primal
     int status;       // -1 running, 0 converged, 1 max_iter, 2 line-search failure, 3 inertia failure
     int iter, n_ls_fail, n_ic, consec_fail;

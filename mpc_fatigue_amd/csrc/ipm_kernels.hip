@@ -636,31 +636,70 @@ struct MeritOut {
 };
 
 
+// Block reductions over NT threads (NT / 64 waves): NMX maxima and NSM sums at once; every thread
+// gets the results.  red: LDS scratch of (NMX + NSM) * (NT / 64) doubles, free on entry.
+template <int NT, int NMX, int NSM>
+__device__ __forceinline__ void block_reduce(double *mx, double *sm, double *red) {
+    constexpr int NW = NT / 64;
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NMX; i++) mx[i] = wave_max(mx[i]);
+#pragma unroll
+    for (int i = 0; i < NSM; i++) sm[i] = wave_sum(sm[i]);
+    __syncthreads();  // red is free: earlier readers are done
+    if ((t & 63) == 0) {
+#pragma unroll
+        for (int i = 0; i < NMX; i++) red[i * NW + (t >> 6)] = mx[i];
+#pragma unroll
+        for (int i = 0; i < NSM; i++) red[(NMX + i) * NW + (t >> 6)] = sm[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NMX; i++) {
+        double r = red[i * NW];
+        for (int w = 1; w < NW; w++) r = fmax(r, red[i * NW + w]);
+        mx[i] = r;
+    }
+#pragma unroll
+    for (int i = 0; i < NSM; i++) {
+        double r = red[(NMX + i) * NW];
+        for (int w = 1; w < NW; w++) r += red[(NMX + i) * NW + w];
+        sm[i] = r;
+    }
+}
+template <int NT> __device__ __forceinline__ double block_max(double v, double *red) {
+    double mx[1] = {v};
+    block_reduce<NT, 1, 0>(mx, nullptr, red);
+    return mx[0];
+}
+template <int NT> __device__ __forceinline__ double block_sum(double v, double *red) {
+    double sm[1] = {v};
+    block_reduce<NT, 0, 1>(nullptr, sm, red);
+    return sm[0];
+}
+
 template <int NJ, int NF, int NL>
 // One interior-point iteration = k_eval_node + three per-problem launches (one wave per
 // problem each; a launch boundary lets each phase have its own register budget):
 //   k_ipm_pre  : optimality error, convergence test, barrier update, barrier Sigma / gradients
 //   k_ipm_kkt  : inertia-corrected Riccati recursion, forward sweep, step recovery
 //   k_ipm_post : fraction to the boundary, merit line search, update
-// Scalars that cross a boundary travel in ProbState (mu, nu, tau_fb, pcorr, regularisation).
-__global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+// Scalars that cross a boundary travel in ProbState (mu, nu, tau_fb, regularisation, step bounds,
+// directional derivative and curvature).
+__global__ __launch_bounds__(256) void k_ipm_pre(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
     constexpr int n = NJ, nf = NF, nl = NL;
     constexpr int NV = 2 * NJ + NF;
     constexpr int NFA = NF > 0 ? NF : 1;
     constexpr int NLA = NL > 0 ? NL : 1;
     constexpr int MB = 3 * NJ + NF + NL;
-    __shared__ ModelLds<NJ> Ml;
-    const DevModel &M = Ml.get();
-    __shared__ DevFrame F;
-    __shared__ int perm[MB], piv[MB];
+    constexpr int NT = 256;  // a block per problem (element loops and block reductions)
+    __shared__ double red[8 * (NT / 64)];
     const int lane = threadIdx.x;
     if ((int)blockIdx.x >= *A.nrun) return;
     const int b = A.list[blockIdx.x];
     ProbState st = A.st[b];
     if (st.status != ST_RUNNING) return;
-    Ml.load(Mg);
-    stage_lds(&F, Fg);
     __shared__ double Bnd[4 * NJ];  // q_lo, q_hi, qd_lo, qd_hi (kernel-argument arrays read per element)
     if (lane < NJ) {
         Bnd[lane] = C.q_lo[lane];
@@ -695,12 +734,12 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
     const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
     double mu = st.mu, nu = st.nu;
-    constexpr int UB = 4;  // element-loop chunk (see the optimality-error phase)
+    constexpr int UB = 2;  // element-loop chunk (see the optimality-error phase)
     auto finish = [&](int status) {
         STAMP_FLUSH;
         double f = 0.0;
-        for (int k = lane; k < N; k += 64) f += cost[k];
-        f = wave_sum(f);
+        for (int k = lane; k < N; k += NT) f += cost[k];
+        f = block_sum<NT>(f, red);
         if (lane == 0) {
             st.status = status;
             st.obj = f;
@@ -724,11 +763,11 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
         sum_bmult += z;
         n_bmult++;
     };
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {  // q rows, k = 1..N
+    for (int e0 = lane; e0 < N * n; e0 += NT * UB) {  // q rows, k = 1..N
         double r[UB], x[UB], zl[UB], zu[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
+            const int e = min(e0 + NT * u, N * n - 1);
             const int k = e / n + 1, j = e % n, i = k * n + j, kk = min(k, N - 1);
             double a = gf[kk * NV + j] + yc[kk * n + j] - yc[(k - 1) * n + j];
 #pragma unroll
@@ -743,7 +782,7 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
         }
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
+            const int e = e0 + NT * u;
             if (e < N * n) {
                 const int j = e % n;
                 dinf = fmax(dinf, fabs(r[u]));
@@ -752,11 +791,11 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
             }
         }
     }
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {  // qd rows (k >= 1), torque rows, continuity
+    for (int e0 = lane; e0 < N * n; e0 += NT * UB) {  // qd rows (k >= 1), torque rows, continuity
         double r[UB], x[UB], zl[UB], zu[UB], r2[UB], xs[UB], vl[UB], vu[UB], lo[UB], hi[UB], pt[UB], pc[UB], ydv[UB], ycv[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
+            const int e = min(e0 + NT * u, N * n - 1);
             const int k = e / n, j = e % n;
             double a = gf[k * NV + n + j] + h * yc[e];
 #pragma unroll
@@ -771,7 +810,7 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
         }
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
+            const int e = e0 + NT * u;
             if (e < N * n) {
                 const int k = e / n, j = e % n;
                 if (k > 0) {
@@ -791,11 +830,11 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
             }
         }
     }
-    for (int e0 = lane; e0 < N * nf; e0 += 64 * UB) {  // force rows
+    for (int e0 = lane; e0 < N * nf; e0 += NT * UB) {  // force rows
         double r[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * nf - 1);
+            const int e = min(e0 + NT * u, N * nf - 1);
             const int k = e / nf, a = e % nf;
             double v = gf[k * NV + 2 * n + a];
 #pragma unroll
@@ -804,25 +843,28 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
         }
 #pragma unroll
         for (int u = 0; u < UB; u++)
-            if (e0 + 64 * u < N * nf) dinf = fmax(dinf, fabs(r[u]));
+            if (e0 + NT * u < N * nf) dinf = fmax(dinf, fabs(r[u]));
     }
-    for (int e0 = lane; e0 < N * nl; e0 += 64 * UB) {  // line rows
+    for (int e0 = lane; e0 < N * nl; e0 += NT * UB) {  // line rows
         double lv[UB], yv[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * nl - 1);
+            const int e = min(e0 + NT * u, N * nl - 1);
             lv[u] = line[e];
             yv[u] = yl[e];
         }
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
+            const int e = e0 + NT * u;
             if (e < N * nl && LINE_ON(e / nl)) { pinf = fmax(pinf, fabs(lv[u])); sum_mult += fabs(yv[u]); n_mult++; }
         }
     }
-    dinf = wave_max(dinf); pinf = wave_max(pinf); cinf0 = wave_max(cinf0); cinfm = wave_max(cinfm);
-    sum_mult = wave_sum(sum_mult); sum_bmult = wave_sum(sum_bmult);
-    n_mult = wave_sum_i(n_mult); n_bmult = wave_sum_i(n_bmult);
+    {
+        double mx[4] = {dinf, pinf, cinf0, cinfm}, sm[4] = {sum_mult, sum_bmult, (double)n_mult, (double)n_bmult};
+        block_reduce<NT, 4, 4>(mx, sm, red);
+        dinf = mx[0]; pinf = mx[1]; cinf0 = mx[2]; cinfm = mx[3];
+        sum_mult = sm[0]; sum_bmult = sm[1]; n_mult = (int)sm[2]; n_bmult = (int)sm[3];
+    }
     const double sd = fmax(s_max, (sum_mult + sum_bmult) / fmax(1.0, (double)(n_mult + n_bmult))) / s_max;
     const double sc = fmax(s_max, sum_bmult / fmax(1.0, (double)n_bmult)) / s_max;
     const double E0 = fmax(fmax(dinf / sd, pinf), cinf0 / sc);
@@ -830,8 +872,8 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
 #ifdef MF_TRACE
     {
         double f = 0.0;
-        for (int k = lane; k < N; k += 64) f += cost[k];
-        f = wave_sum(f);
+        for (int k = lane; k < N; k += NT) f += cost[k];
+        f = block_sum<NT>(f, red);
         TRACE(14, f);
     }
 #endif
@@ -845,14 +887,14 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
         if (mnew >= mu) break;
         mu = mnew;
         double cm = 0.0;
-        for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        for (int e0 = lane; e0 < N * n; e0 += NT * UB) {
             double cp[6][UB];
 #pragma unroll
             for (int u = 0; u < UB; u++) {
-                const int e = min(e0 + 64 * u, N * n - 1);
+                const int e = min(e0 + NT * u, N * n - 1);
                 const int i = e + n, j = e % n;
                 const double xq = q[i], xd = qd[e], xs = s[e], l = tlo[e], hh = thi[e];
-                const bool in = e0 + 64 * u < N * n, kq = e / n > 0;
+                const bool in = e0 + NT * u < N * n, kq = e / n > 0;
                 cp[0][u] = (in && hasb(QLO[j])) ? zqL[i] * (xq - QLO[j]) : NAN;
                 cp[1][u] = (in && hasb(QHI[j])) ? zqU[i] * (QHI[j] - xq) : NAN;
                 cp[2][u] = (in && kq && hasb(DLO[j])) ? zdL[e] * (xd - DLO[j]) : NAN;
@@ -866,7 +908,7 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
                 for (int p = 0; p < 6; p++)
                     if (!isnan(cp[p][u])) cm = fmax(cm, fabs(cp[p][u] - mu));
         }
-        cinfm = wave_max(cm);
+        cinfm = block_max<NT>(cm, red);
         Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
     }
     const double tau_fb = fmax(tau_min, 1.0 - mu);
@@ -874,16 +916,16 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
     STAMP(0);
 
     // ---------------- barrier Sigma and gradients
-    for (int e0 = lane; e0 < (N + 1) * n; e0 += 64 * UB) {
+    for (int e0 = lane; e0 < (N + 1) * n; e0 += NT * UB) {
         double x[UB], zl[UB], zu[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, (N + 1) * n - 1);
+            const int e = min(e0 + NT * u, (N + 1) * n - 1);
             x[u] = q[e]; zl[u] = zqL[e]; zu[u] = zqU[e];
         }
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
+            const int e = e0 + NT * u;
             if (e < (N + 1) * n) {
                 const int k = e / n, j = e % n;
                 double sx = 0, gp = 0;
@@ -896,17 +938,17 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
             }
         }
     }
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+    for (int e0 = lane; e0 < N * n; e0 += NT * UB) {
         double x[UB], zl[UB], zu[UB], xs[UB], vl[UB], vu[UB], lo[UB], hi[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
+            const int e = min(e0 + NT * u, N * n - 1);
             x[u] = qd[e]; zl[u] = zdL[e]; zu[u] = zdU[e];
             xs[u] = s[e]; vl[u] = vL[e]; vu[u] = vU[e]; lo[u] = tlo[e]; hi[u] = thi[e];
         }
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
+            const int e = e0 + NT * u;
             if (e < N * n) {
                 const int k = e / n, j = e % n;
                 double sx = 0, gp = 0, gs = 0;
@@ -934,6 +976,337 @@ __global__ __launch_bounds__(64) void k_ipm_pre(const DevModel *__restrict__ Mg,
         A.st[b] = st;
     }
 #undef TACT
+}
+
+// ---------------- per-stage inputs of the Riccati recursion
+// For every stage k at once: g_k (NV), c_k = q_k + h qd_k - q_{k+1} (NJ), e_k = line_{k+1} +
+// Jl_{k+1} c_k, dD_k = D_tau(dw, dc) - Sigma_s (NJ), into stg (stage k contiguous, SG doubles), and
+// y_tau + D_tau r_tau (N x NJ) into the scratch behind it.  NT threads of one horizon (tid < NT)
+// stride the elements; `sync` orders the phases (a wave: s_waitcnt; a block: __syncthreads).
+// k_kkt_prep runs it for the first inertia try with a whole block per horizon; k_ipm_kkt reruns
+// it in its own wave only when a retry changes (dw, dc).  Same per-element arithmetic either way.
+template <int NJ, int NF, int NL, int NT, class Sync>
+__device__ __forceinline__ void prep_stage_inputs(const OcpConst &C, const IpmArrays &A, int b, int tid, double dwv,
+                                                  double dcv, Sync sync) {
+    constexpr int n = NJ, nl = NL, NV = 2 * NJ + NF;
+    constexpr int NLA2 = NL > 0 ? NL : 1;
+    constexpr int SG = NV + 2 * NJ + NLA2;
+    constexpr int UB = 2;
+    const IpmSizes S = ipm_sizes(C);
+    const int N = C.N;
+    const double h = C.h;
+    const double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *s = A.s + b * S.u;
+    const double *yc = A.yc + b * S.u, *yl = A.yl + b * S.l, *yd = A.yd + b * S.u;
+    const double *tau = A.tau + b * S.u, *Jt = A.Jt + b * S.jt, *line = A.line + b * S.l, *Jl = A.Jl + b * S.jl;
+    const double *gf = A.gf + b * S.gf;
+    const double *gphq = A.gphq + b * S.q, *gphd = A.gphd + b * S.u, *Ss = A.Ss + b * S.u, *gphs = A.gphs + b * S.u;
+    const double *tlo = A.tau_lo, *thi = A.tau_hi;
+    double *stg = A.stg + b * S.stg;
+    double *wst = stg + (size_t)N * SG;
+    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
+        double ydv[UB], ssv[UB], tv[UB], sv[UB], gv[UB], lo[UB], hi[UB], qa[UB], qdv[UB], qb[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * n - 1);
+            ydv[u] = yd[e]; ssv[u] = Ss[e]; tv[u] = tau[e]; sv[u] = s[e]; gv[u] = gphs[e];
+            lo[u] = tlo[e]; hi[u] = thi[e]; qa[u] = q[e]; qdv[u] = qd[e]; qb[u] = q[e + n];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + NT * u;
+            if (e < N * n) {
+                double wv_ = ydv[u], dD = 0.0;
+                if (hasb(lo[u]) || hasb(hi[u])) {
+                    const double sg = ssv[u] + dwv;
+                    const double Dd = sg / (1.0 + dcv * sg);
+                    wv_ += Dd * ((tv[u] - sv[u]) + (gv[u] - ydv[u]) / sg);
+                    dD = Dd - ssv[u];
+                }
+                const int k = e / n, j = e % n;
+                wst[e] = wv_;
+                stg[k * SG + NV + NJ + NLA2 + j] = dD;
+                stg[k * SG + NV + j] = qa[u] + h * qdv[u] - qb[u];
+            }
+        }
+    }
+    sync();  // wst / c_k are read back by other threads
+    for (int e0 = tid; e0 < N * NV; e0 += NT * UB) {
+        double g[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * NV - 1);
+            const int k = e / NV, v = e % NV;
+            const int vq = v < n ? v : 0, vd = (v >= n && v < 2 * n) ? v - n : 0;
+            double a = gf[e];
+            const double *Jtk = Jt + (size_t)k * n * NV;
+#pragma unroll
+            for (int jj = 0; jj < NJ; jj++) a += Jtk[jj * NV + v] * wst[k * n + jj];
+            double aq = gphq[k * n + vq] + yc[k * n + vq] - (k > 0 ? yc[(k > 0 ? k - 1 : 0) * n + vq] : 0.0);
+#pragma unroll
+            for (int l = 0; l < NL; l++) aq += Jl[(k * nl + l) * n + vq] * yl[k * nl + l];
+            const double ad = gphd[k * n + vd] + h * yc[k * n + vd];
+            g[u] = a + (v < n ? aq : (v < 2 * n ? ad : 0.0));
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++)
+            if (e0 + NT * u < N * NV) stg[((e0 + NT * u) / NV) * SG + (e0 + NT * u) % NV] = g[u];
+    }
+    for (int e0 = tid; e0 < N * nl; e0 += NT * UB) {
+        double a[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * nl - 1);
+            const int k = e / nl, l = e % nl, k1 = min(k + 1, N - 1);
+            double v = line[k1 * nl + l];
+#pragma unroll
+            for (int i = 0; i < NJ; i++) v += Jl[((size_t)k1 * nl + l) * n + i] * stg[k * SG + NV + i];
+            a[u] = (LINE_ON(k + 1) && k + 1 <= N - 1) ? v : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + NT * u;
+            if (e < N * nl) stg[(e / nl) * SG + NV + NJ + e % nl] = a[u];
+        }
+    }
+    sync();  // the stage loop reads the blocks back
+}
+
+// Regularisation of an iteration's first inertia try (IPOPT's rule: a third of the last
+// successful perturbation, dropped below 1e-8; k_ipm_kkt and k_kkt_prep must agree on it).
+__device__ __forceinline__ void kkt_first_try(const ProbState &st, int &tier, double &reg, double &dw, double &dFr) {
+    tier = st.reg_tier;
+    reg = (st.reg_tier == 0) ? 0.0 : st.reg_last / 3.0;
+    if (st.reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
+    dw = (tier == 2) ? reg : 0.0;
+    dFr = (tier == 1) ? reg : 0.0;
+}
+
+// The per-stage inputs of the first inertia try, one 256-thread block per running horizon: element
+// work that is latency-bound inside k_ipm_kkt's single wave runs here at full occupancy.
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(256) void k_kkt_prep(OcpConst C, IpmArrays A, int batch) {
+    if ((int)blockIdx.x >= *A.nrun) return;
+    const int b = A.list[blockIdx.x];
+    const ProbState st = A.st[b];
+    if (st.status != ST_RUNNING) return;
+    int tier;
+    double reg, dw, dFr;
+    kkt_first_try(st, tier, reg, dw, dFr);
+    prep_stage_inputs<NJ, NF, NL, 256>(C, A, b, threadIdx.x, dw, 0.0, [] { __syncthreads(); });
+}
+
+// Step recovery after k_ipm_kkt's sweeps, one 256-thread block per running horizon:
+// dyc_k = P_{k+1} dx_{k+1} + p_{k+1} + Jl_{k+1}^T dyl_{k+1} for every stage, dyd, ds, the bound
+// multiplier steps and the step-curvature correction pcorr (-> k_ipm_post).
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, int batch) {
+    constexpr int n = NJ, nl = NL;
+    constexpr int NV = 2 * NJ + NF;
+    constexpr int NFA = NF > 0 ? NF : 1;
+    constexpr int MB = 3 * NJ + NF + NL;
+    constexpr int NU = NJ + NF;
+    constexpr int NT = 256, UB = 2;
+    if ((int)blockIdx.x >= *A.nrun) return;
+    const int b = A.list[blockIdx.x];
+    const ProbState st = A.st[b];
+    if (st.status != ST_RUNNING) return;
+    const int tid = threadIdx.x;
+    __shared__ double Bnd[4 * NJ];
+    __shared__ double red[4 * (NT / 64)];
+    if (tid < NJ) {
+        Bnd[tid] = C.q_lo[tid];
+        Bnd[NJ + tid] = C.q_hi[tid];
+        Bnd[2 * NJ + tid] = C.qd_lo[tid];
+        Bnd[3 * NJ + tid] = C.qd_hi[tid];
+    }
+    __syncthreads();
+    const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
+    const IpmSizes S = ipm_sizes(C);
+    const int N = C.N;
+    const double mu = st.mu, dw = st.kkt_dw, dc = st.kkt_dc;
+    const double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *s = A.s + b * S.u, *yd = A.yd + b * S.u;
+    const double *zqL = A.zqL + b * S.q, *zqU = A.zqU + b * S.q, *zdL = A.zdL + b * S.u, *zdU = A.zdU + b * S.u;
+    const double *vL = A.vL + b * S.u, *vU = A.vU + b * S.u;
+    const double *dq = A.dq + b * S.q, *dqd = A.dqd + b * S.u, *dF = A.dF + b * S.f, *dyl = A.dyl + b * S.l;
+    double *ds = A.ds + b * S.u, *dyc = A.dyc + b * S.u, *dyd = A.dyd + b * S.u;
+    double *dzqL = A.dzqL + b * S.q, *dzqU = A.dzqU + b * S.q, *dzdL = A.dzdL + b * S.u, *dzdU = A.dzdU + b * S.u;
+    double *dvL = A.dvL + b * S.u, *dvU = A.dvU + b * S.u;
+    const double *tau = A.tau + b * S.u, *Jt = A.Jt + b * S.jt, *Jl = A.Jl + b * S.jl;
+    const double *Ss = A.Ss + b * S.u, *gphs = A.gphs + b * S.u;
+    const double *W = A.W + b * S.w, *gf = A.gf + b * S.gf;
+    const double *Sxq = A.Sxq + b * S.q, *gphq = A.gphq + b * S.q, *gphd = A.gphd + b * S.u;
+    const double *G = A.G + b * S.G, *wv = A.wv + b * S.wv;
+    const double *tlo = A.tau_lo, *thi = A.tau_hi;
+    // fraction to the boundary (primal ap, bound multipliers az), accumulated where the steps are formed
+    const double tau_fb = st.tau_fb;
+    double ap = 1.0, az = 1.0;
+    auto ftbL = [&](double x, double dx, double lo, double &a) { if (dx < 0) a = fmin(a, -tau_fb * (x - lo) / dx); };
+    auto ftbU = [&](double x, double dx, double hi, double &a) { if (dx > 0) a = fmin(a, tau_fb * (hi - x) / dx); };
+    auto ftbZ = [&](double z, double dz, double &a) { if (dz < 0) a = fmin(a, -tau_fb * z / dz); };
+    // dyc_k for every stage
+    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
+        double a[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * n - 1);
+            const int k = e / n, j = e % n;
+            const double *Pj = G + (size_t)k * MB * n + (size_t)(NU + NL + j) * n;
+            double v = wv[(size_t)k * MB + NU + NL + j];
+#pragma unroll
+            for (int i = 0; i < NJ; i++) v += Pj[i] * dq[(k + 1) * n + i];
+            const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
+            const int k1 = min(k + 1, N - 1);
+#pragma unroll
+            for (int l = 0; l < NL; l++) {
+                const double jl = Jl[((size_t)k1 * nl + l) * n + j], yl1 = dyl[k1 * nl + l];
+                if (con1) v += jl * yl1;  // (contracted like the sweep's own update: same round-off)
+            }
+            a[u] = v;
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++)
+            if (e0 + NT * u < N * n) dyc[e0 + NT * u] = a[u];
+    }
+    // dyd, ds; pcorr = sum Sigma_s (ds^2 - (J dx)^2) turns p^T H0 p into the oracle's p^T (W + Sigma) p
+    double pcorr = 0.0;
+    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
+        double jdx[UB], ssv[UB], gv[UB], ydv[UB], tv[UB], sv[UB], lo[UB], hi[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * n - 1);
+            const int k = e / n, j = e % n;
+            const double *Jtk = Jt + ((size_t)k * n + j) * NV;
+            double a = 0.0;
+#pragma unroll
+            for (int v = 0; v < NJ; v++) a += Jtk[v] * dq[k * n + v] + Jtk[n + v] * dqd[k * n + v];
+#pragma unroll
+            for (int f = 0; f < NF; f++) a += Jtk[2 * n + f] * dF[k * NFA + f];
+            jdx[u] = a;
+            ssv[u] = Ss[e]; gv[u] = gphs[e]; ydv[u] = yd[e]; tv[u] = tau[e]; sv[u] = s[e];
+            lo[u] = tlo[e]; hi[u] = thi[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + NT * u;
+            if (e < N * n) {
+                double dydv = 0.0, dsv = 0.0;
+                if (hasb(lo[u]) || hasb(hi[u])) {
+                    const double sg = ssv[u] + dw, Dd = sg / (1.0 + dc * sg);
+                    const double rs = gv[u] - ydv[u], rd = tv[u] - sv[u];
+                    dydv = Dd * (jdx[u] + rd + rs / sg);
+                    dsv = (dydv - rs) / sg;
+                    pcorr += ssv[u] * (dsv * dsv - jdx[u] * jdx[u]);
+                }
+                dyd[e] = dydv;
+                ds[e] = dsv;
+            }
+        }
+    }
+    for (int e0 = tid; e0 < (N + 1) * n; e0 += NT * UB) {
+        double x[UB], dx[UB], zl[UB], zu[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, (N + 1) * n - 1);
+            x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; zu[u] = zqU[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + NT * u;
+            if (e < (N + 1) * n) {
+                const int k = e / n, j = e % n;
+                double a = 0, bb = 0;
+                if (k > 0) {
+                    if (hasb(QLO[j])) a = mu / (x[u] - QLO[j]) - zl[u] - zl[u] / (x[u] - QLO[j]) * dx[u];
+                    if (hasb(QHI[j])) bb = mu / (QHI[j] - x[u]) - zu[u] + zu[u] / (QHI[j] - x[u]) * dx[u];
+                    if (hasb(QLO[j])) { ftbL(x[u], dx[u], QLO[j], ap); ftbZ(zl[u], a, az); }
+                    if (hasb(QHI[j])) { ftbU(x[u], dx[u], QHI[j], ap); ftbZ(zu[u], bb, az); }
+                }
+                dzqL[e] = a; dzqU[e] = bb;
+            }
+        }
+    }
+    __syncthreads();  // ds is read back by other threads
+    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
+        double x[UB], dx[UB], zl[UB], zu[UB], xs[UB], dxs[UB], vl[UB], vu[UB], lo[UB], hi[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * n - 1);
+            x[u] = qd[e]; dx[u] = dqd[e]; zl[u] = zdL[e]; zu[u] = zdU[e];
+            xs[u] = s[e]; dxs[u] = ds[e]; vl[u] = vL[e]; vu[u] = vU[e]; lo[u] = tlo[e]; hi[u] = thi[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + NT * u;
+            if (e < N * n) {
+                const int k = e / n, j = e % n;
+                double a = 0, bb = 0, c = 0, d = 0;
+                if (k > 0) {
+                    if (hasb(DLO[j])) a = mu / (x[u] - DLO[j]) - zl[u] - zl[u] / (x[u] - DLO[j]) * dx[u];
+                    if (hasb(DHI[j])) bb = mu / (DHI[j] - x[u]) - zu[u] + zu[u] / (DHI[j] - x[u]) * dx[u];
+                }
+                if (hasb(lo[u])) c = mu / (xs[u] - lo[u]) - vl[u] - vl[u] / (xs[u] - lo[u]) * dxs[u];
+                if (hasb(hi[u])) d = mu / (hi[u] - xs[u]) - vu[u] + vu[u] / (hi[u] - xs[u]) * dxs[u];
+                dzdL[e] = a; dzdU[e] = bb; dvL[e] = c; dvU[e] = d;
+                if (k > 0) {
+                    if (hasb(DLO[j])) { ftbL(x[u], dx[u], DLO[j], ap); ftbZ(zl[u], a, az); }
+                    if (hasb(DHI[j])) { ftbU(x[u], dx[u], DHI[j], ap); ftbZ(zu[u], bb, az); }
+                }
+                if (hasb(lo[u])) { ftbL(xs[u], dxs[u], lo[u], ap); ftbZ(vl[u], c, az); }
+                if (hasb(hi[u])) { ftbU(xs[u], dxs[u], hi[u], ap); ftbZ(vu[u], d, az); }
+            }
+        }
+    }
+    // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx = pcorr + dx^T H0 dx + the q_N barrier term;
+    // thread e covers row v of node k's H0 (stored as its lower triangle)
+    double gdot = 0.0, pHp = pcorr;
+    for (int e0 = tid; e0 < N * NV; e0 += NT * 2) {
+        double acc[2], gd[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int e = min(e0 + NT * u, N * NV - 1);
+            const int k = e / NV, v = e % NV;
+            double dx[NV];
+#pragma unroll
+            for (int j = 0; j < NJ; j++) { dx[j] = dq[k * n + j]; dx[NJ + j] = dqd[k * n + j]; }
+#pragma unroll
+            for (int a = 0; a < NF; a++) dx[2 * NJ + a] = dF[k * NFA + a];
+            const double *Wr = W + (size_t)k * NV * NV + (size_t)v * NV;
+            double a = 0.0, dv = 0.0;
+#pragma unroll
+            for (int w = 0; w < NV; w++) {
+                const double hw = Wr[w];  // loaded unconditionally; the upper part is stale, never used
+                a += (w < v ? 2.0 * hw : (w == v ? hw : 0.0)) * dx[w];
+                if (w == v) dv = dx[w];
+            }
+            acc[u] = a * dv;
+            gd[u] = gf[e] * dv;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            if (e0 + NT * u < N * NV) { pHp += acc[u]; gdot += gd[u]; }
+    }
+    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
+        double g1[UB], g2[UB], g3[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * n - 1);
+            const double dqv = dq[e + n];
+            g1[u] = gphd[e] * dqd[e] + gphs[e] * ds[e];
+            g2[u] = gphq[e + n] * dqv;
+            g3[u] = (e + n >= N * n) ? Sxq[e + n] * dqv * dqv : 0.0;  // q_N (stages k < N carry Sigma_x in H0)
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++)
+            if (e0 + NT * u < N * n) { gdot += g1[u] + g2[u]; pHp += g3[u]; }
+    }
+    double mx[2] = {-ap, -az}, sm[2] = {gdot, pHp};
+    block_reduce<NT, 2, 2>(mx, sm, red);
+    if (tid == 0) {
+        A.st[b].ap = -mx[0];
+        A.st[b].az = -mx[1];
+        A.st[b].gdot = sm[0];
+        A.st[b].pHp = sm[1];
+    }
 }
 
 template <int NJ, int NF, int NL>
@@ -1047,83 +1420,16 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
     double *wst = stg + (size_t)N * SG;
     __shared__ double Stg[SG];  // stage k's block, staged from a register prefetch
     auto prep_stages = [&](double dwv, double dcv) {
-        for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
-            double ydv[UB], ssv[UB], tv[UB], sv[UB], gv[UB], lo[UB], hi[UB], qa[UB], qdv[UB], qb[UB];
-#pragma unroll
-            for (int u = 0; u < UB; u++) {
-                const int e = min(e0 + 64 * u, N * n - 1);
-                ydv[u] = yd[e]; ssv[u] = Ss[e]; tv[u] = tau[e]; sv[u] = s[e]; gv[u] = gphs[e];
-                lo[u] = tlo[e]; hi[u] = thi[e]; qa[u] = q[e]; qdv[u] = qd[e]; qb[u] = q[e + n];
-            }
-#pragma unroll
-            for (int u = 0; u < UB; u++) {
-                const int e = e0 + 64 * u;
-                if (e < N * n) {
-                    double wv_ = ydv[u], dD = 0.0;
-                    if (hasb(lo[u]) || hasb(hi[u])) {
-                        const double sg = ssv[u] + dwv;
-                        const double Dd = sg / (1.0 + dcv * sg);
-                        wv_ += Dd * ((tv[u] - sv[u]) + (gv[u] - ydv[u]) / sg);
-                        dD = Dd - ssv[u];
-                    }
-                    const int k = e / n, j = e % n;
-                    wst[e] = wv_;
-                    stg[k * SG + NV + NJ + NLA2 + j] = dD;
-                    stg[k * SG + NV + j] = qa[u] + h * qdv[u] - qb[u];
-                }
-            }
-        }
-        wave_mem_sync();  // wst / c_k are read back by other lanes
-        for (int e0 = lane; e0 < N * NV; e0 += 64 * UB) {
-            double g[UB];
-#pragma unroll
-            for (int u = 0; u < UB; u++) {
-                const int e = min(e0 + 64 * u, N * NV - 1);
-                const int k = e / NV, v = e % NV;
-                const int vq = v < n ? v : 0, vd = (v >= n && v < 2 * n) ? v - n : 0;
-                double a = gf[e];
-                const double *Jtk = Jt + (size_t)k * n * NV;
-#pragma unroll
-                for (int jj = 0; jj < NJ; jj++) a += Jtk[jj * NV + v] * wst[k * n + jj];
-                double aq = gphq[k * n + vq] + yc[k * n + vq] - (k > 0 ? yc[(k > 0 ? k - 1 : 0) * n + vq] : 0.0);
-#pragma unroll
-                for (int l = 0; l < NL; l++) aq += Jl[(k * nl + l) * n + vq] * yl[k * nl + l];
-                const double ad = gphd[k * n + vd] + h * yc[k * n + vd];
-                g[u] = a + (v < n ? aq : (v < 2 * n ? ad : 0.0));
-            }
-#pragma unroll
-            for (int u = 0; u < UB; u++)
-                if (e0 + 64 * u < N * NV) stg[((e0 + 64 * u) / NV) * SG + (e0 + 64 * u) % NV] = g[u];
-        }
-        for (int e0 = lane; e0 < N * nl; e0 += 64 * UB) {
-            double a[UB];
-#pragma unroll
-            for (int u = 0; u < UB; u++) {
-                const int e = min(e0 + 64 * u, N * nl - 1);
-                const int k = e / nl, l = e % nl, k1 = min(k + 1, N - 1);
-                double v = line[k1 * nl + l];
-#pragma unroll
-                for (int i = 0; i < NJ; i++) v += Jl[((size_t)k1 * nl + l) * n + i] * stg[k * SG + NV + i];
-                a[u] = (LINE_ON(k + 1) && k + 1 <= N - 1) ? v : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < UB; u++) {
-                const int e = e0 + 64 * u;
-                if (e < N * nl) stg[(e / nl) * SG + NV + NJ + e % nl] = a[u];
-            }
-        }
-        wave_mem_sync();  // the stage loop reads the blocks back
+        prep_stage_inputs<NJ, NF, NL, 64>(C, A, b, lane, dwv, dcv, [] { wave_mem_sync(); });
     };
-    double dw = 0.0, dc = 0.0, dFr = 0.0;
+    double dw, dc = 0.0, dFr, reg;
     const int reg_tier0 = st.reg_tier;
     const double reg_last0 = st.reg_last;
-    int tier = reg_tier0, step_no = 0;
-    double reg = (reg_tier0 == 0) ? 0.0 : reg_last0 / 3.0;
-    if (reg_tier0 != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
-    if (tier == 1) dFr = reg; else if (tier == 2) dw = reg;
+    int tier, step_no = 0;
+    kkt_first_try(st, tier, reg, dw, dFr);
     bool factor_ok = false;
     int ntries = 0;
-    double prep_dw = NAN, prep_dc = NAN;
+    double prep_dw = dw, prep_dc = 0.0;  // k_kkt_prep wrote the first try's stage inputs
     for (int tries = 0; tries < 60; tries++) {
         ntries++;
         bool ok = true, zero = false;
@@ -1430,124 +1736,12 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
         }
     }
     for (int j = lane; j < n; j += 64) dq[N * n + j] = xsv[j];
-    wave_mem_sync();  // dq_{k+1}, dyl_{k+1} are read back by other lanes
-    // ---------------- forward sweep, parallel part: dyc_k for every stage
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
-        double a[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
-            const int k = e / n, j = e % n;
-            const double *Pj = G + (size_t)k * MB * n + (size_t)(NU + NL + j) * n;
-            double v = wv[(size_t)k * MB + NU + NL + j];
-#pragma unroll
-            for (int i = 0; i < NJ; i++) v += Pj[i] * dq[(k + 1) * n + i];
-            const bool con1 = (nl > 0) && LINE_ON(k + 1) && (k + 1 <= N - 1);
-            const int k1 = min(k + 1, N - 1);
-#pragma unroll
-            for (int l = 0; l < NL; l++) {
-                const double jl = Jl[((size_t)k1 * nl + l) * n + j], yl1 = dyl[k1 * nl + l];
-                if (con1) v += jl * yl1;  // (contracted like the sweep's own update: same round-off)
-            }
-            a[u] = v;
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++)
-            if (e0 + 64 * u < N * n) dyc[e0 + 64 * u] = a[u];
-    }
-    __threadfence_block();
-    __syncthreads();
-
-    // ---------------- dyd, ds, dz, dv
-    double pcorr = 0.0;  // sum Sigma_s (ds^2 - (J dx)^2): turns p^T H0 p into the oracle's p^T (W + Sigma) p
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
-        double jdx[UB], ssv[UB], gv[UB], ydv[UB], tv[UB], sv[UB], lo[UB], hi[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
-            const int k = e / n, j = e % n;
-            const double *Jtk = Jt + ((size_t)k * n + j) * NV;
-            double a = 0.0;
-#pragma unroll
-            for (int v = 0; v < NJ; v++) a += Jtk[v] * dq[k * n + v] + Jtk[n + v] * dqd[k * n + v];
-#pragma unroll
-            for (int f = 0; f < NF; f++) a += Jtk[2 * n + f] * dF[k * NFA + f];
-            jdx[u] = a;
-            ssv[u] = Ss[e]; gv[u] = gphs[e]; ydv[u] = yd[e]; tv[u] = tau[e]; sv[u] = s[e];
-            lo[u] = tlo[e]; hi[u] = thi[e];
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
-            if (e < N * n) {
-                double dydv = 0.0, dsv = 0.0;
-                if (hasb(lo[u]) || hasb(hi[u])) {
-                    const double sg = ssv[u] + dw, Dd = sg / (1.0 + dc * sg);
-                    const double rs = gv[u] - ydv[u], rd = tv[u] - sv[u];
-                    dydv = Dd * (jdx[u] + rd + rs / sg);
-                    dsv = (dydv - rs) / sg;
-                    pcorr += ssv[u] * (dsv * dsv - jdx[u] * jdx[u]);
-                }
-                dyd[e] = dydv;
-                ds[e] = dsv;
-            }
-        }
-    }
-    for (int e0 = lane; e0 < (N + 1) * n; e0 += 64 * UB) {
-        double x[UB], dx[UB], zl[UB], zu[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, (N + 1) * n - 1);
-            x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; zu[u] = zqU[e];
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
-            if (e < (N + 1) * n) {
-                const int k = e / n, j = e % n;
-                double a = 0, bb = 0;
-                if (k > 0) {
-                    if (hasb(QLO[j])) a = mu / (x[u] - QLO[j]) - zl[u] - zl[u] / (x[u] - QLO[j]) * dx[u];
-                    if (hasb(QHI[j])) bb = mu / (QHI[j] - x[u]) - zu[u] + zu[u] / (QHI[j] - x[u]) * dx[u];
-                }
-                dzqL[e] = a; dzqU[e] = bb;
-            }
-        }
-    }
-    __threadfence_block();
-    __syncthreads();
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
-        double x[UB], dx[UB], zl[UB], zu[UB], xs[UB], dxs[UB], vl[UB], vu[UB], lo[UB], hi[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
-            x[u] = qd[e]; dx[u] = dqd[e]; zl[u] = zdL[e]; zu[u] = zdU[e];
-            xs[u] = s[e]; dxs[u] = ds[e]; vl[u] = vL[e]; vu[u] = vU[e]; lo[u] = tlo[e]; hi[u] = thi[e];
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
-            if (e < N * n) {
-                const int k = e / n, j = e % n;
-                double a = 0, bb = 0, c = 0, d = 0;
-                if (k > 0) {
-                    if (hasb(DLO[j])) a = mu / (x[u] - DLO[j]) - zl[u] - zl[u] / (x[u] - DLO[j]) * dx[u];
-                    if (hasb(DHI[j])) bb = mu / (DHI[j] - x[u]) - zu[u] + zu[u] / (DHI[j] - x[u]) * dx[u];
-                }
-                if (hasb(lo[u])) c = mu / (xs[u] - lo[u]) - vl[u] - vl[u] / (xs[u] - lo[u]) * dxs[u];
-                if (hasb(hi[u])) d = mu / (hi[u] - xs[u]) - vu[u] + vu[u] / (hi[u] - xs[u]) * dxs[u];
-                dzdL[e] = a; dzdU[e] = bb; dvL[e] = c; dvU[e] = d;
-            }
-        }
-    }
-    __threadfence_block();
-    __syncthreads();
-
+    // dyc, dyd, ds, the bound multiplier steps and pcorr: k_kkt_recover (a block per horizon)
     STAMP(3);
-    pcorr = wave_sum(pcorr);
     STAMP_FLUSH;
     if (lane == 0) {
-        st.pcorr = pcorr;
+        st.kkt_dw = dw;
+        st.kkt_dc = dc;
         A.st[b] = st;
     }
 #undef TACT
@@ -1622,52 +1816,8 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         }
     };
     const double tau_fb = st.tau_fb;
-    // ---------------- fraction to boundary
-    double ap = 1.0, az = 1.0;
-    auto ftbL = [&](double x, double dx, double lo, double &a) { if (dx < 0) a = fmin(a, -tau_fb * (x - lo) / dx); };
-    auto ftbU = [&](double x, double dx, double hi, double &a) { if (dx > 0) a = fmin(a, tau_fb * (hi - x) / dx); };
-    auto ftbZ = [&](double z, double dz, double &a) { if (dz < 0) a = fmin(a, -tau_fb * z / dz); };
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {  // q_k, k = 1..N
-        double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1) + n;
-            x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; dzl[u] = dzqL[e]; zu[u] = zqU[e]; dzu[u] = dzqU[e];
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            if (e0 + 64 * u < N * n) {
-                const int j = (e0 + 64 * u) % n;
-                if (hasb(QLO[j])) { ftbL(x[u], dx[u], QLO[j], ap); ftbZ(zl[u], dzl[u], az); }
-                if (hasb(QHI[j])) { ftbU(x[u], dx[u], QHI[j], ap); ftbZ(zu[u], dzu[u], az); }
-            }
-        }
-    }
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
-        double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB], xs[UB], dxs[UB], vl[UB], dvl[UB], vu[UB], dvu[UB], lo[UB], hi[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
-            x[u] = qd[e]; dx[u] = dqd[e]; zl[u] = zdL[e]; dzl[u] = dzdL[e]; zu[u] = zdU[e]; dzu[u] = dzdU[e];
-            xs[u] = s[e]; dxs[u] = ds[e]; vl[u] = vL[e]; dvl[u] = dvL[e]; vu[u] = vU[e]; dvu[u] = dvU[e];
-            lo[u] = tlo[e]; hi[u] = thi[e];
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
-            if (e < N * n) {
-                const int k = e / n, j = e % n;
-                if (k > 0) {
-                    if (hasb(DLO[j])) { ftbL(x[u], dx[u], DLO[j], ap); ftbZ(zl[u], dzl[u], az); }
-                    if (hasb(DHI[j])) { ftbU(x[u], dx[u], DHI[j], ap); ftbZ(zu[u], dzu[u], az); }
-                }
-                if (hasb(lo[u])) { ftbL(xs[u], dxs[u], lo[u], ap); ftbZ(vl[u], dvl[u], az); }
-                if (hasb(hi[u])) { ftbU(xs[u], dxs[u], hi[u], ap); ftbZ(vu[u], dvu[u], az); }
-            }
-        }
-    }
-    ap = wave_min(ap);
-    az = wave_min(az);
+    // ---------------- fraction to boundary (k_kkt_recover)
+    const double ap = st.ap, az = st.az;
     TRACE(9, ap); TRACE(10, az);
 
     // ---------------- merit at the current point, directional derivative, curvature
@@ -1762,51 +1912,8 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         bool ok0;
         merit(0.0, phi0, th0, ok0);
     }
-    // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx; lane e covers row v of node k's W (lower triangle)
-    double gdot = 0, pHp = (lane == 0) ? st.pcorr : 0.0;  // pcorr: whole-wave sum from k_ipm_kkt
-    for (int e0 = lane; e0 < N * NV; e0 += 64 * 2) {
-        double acc[2], gd[2];
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-            const int e = min(e0 + 64 * u, N * NV - 1);
-            const int k = e / NV, v = e % NV;
-            double dx[NV];
-#pragma unroll
-            for (int j = 0; j < NJ; j++) { dx[j] = dq[k * n + j]; dx[NJ + j] = dqd[k * n + j]; }
-#pragma unroll
-            for (int a = 0; a < NF; a++) dx[2 * NJ + a] = dF[k * NFA + a];
-            const double *Wr = W + (size_t)k * NV * NV + (size_t)v * NV;
-            // H0 is stored as its lower triangle: row v's part left of the diagonal counts twice
-            double a = 0.0, dv = 0.0;
-#pragma unroll
-            for (int w = 0; w < NV; w++) {
-                const double hw = Wr[w];  // loaded unconditionally; the upper part is stale, never used
-                a += (w < v ? 2.0 * hw : (w == v ? hw : 0.0)) * dx[w];
-                if (w == v) dv = dx[w];
-            }
-            acc[u] = a * dv;
-            gd[u] = gf[e] * dv;
-        }
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-            if (e0 + 64 * u < N * NV) { pHp += acc[u]; gdot += gd[u]; }
-    }
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
-        double g1[UB], g2[UB], g3[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
-            const double dqv = dq[e + n];
-            g1[u] = gphd[e] * dqd[e] + gphs[e] * ds[e];
-            g2[u] = gphq[e + n] * dqv;
-            g3[u] = (e + n >= N * n) ? Sxq[e + n] * dqv * dqv : 0.0;  // q_N (stages k < N carry Sigma_x in H0)
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++)
-            if (e0 + 64 * u < N * n) { gdot += g1[u] + g2[u]; pHp += g3[u]; }
-    }
-    gdot = wave_sum(gdot);
-    pHp = wave_sum(pHp);
+    // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx (k_kkt_recover)
+    const double gdot = st.gdot, pHp = st.pHp;
     if (th0 > 1e-300) {
         double nreq = (gdot + 0.5 * fmax(pHp, 0.0)) / ((1.0 - rho) * th0);
         if (nu < nreq) nu = nreq + 1.0;
@@ -1840,21 +1947,68 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         st.consec_fail = 0;
     }
 
+    st.alpha = alpha;  // the update itself: k_post_update (a block per horizon)
+    STAMP(6);
+    STAMP_COUNT(10, 1);
+    STAMP_FLUSH;
+    if (lane == 0) {
+        st.iter++;
+        st.mu = mu;
+        st.nu = nu;
+        A.st[b] = st;
+    }
+#undef TACT
+}
+
+
+// The primal-dual update with the step k_ipm_post accepted (alpha) and the bound multipliers' step
+// az, one 256-thread block per running horizon.
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(256) void k_post_update(OcpConst C, IpmArrays A, int batch) {
+    constexpr int n = NJ, nf = NF, nl = NL;
+    constexpr int NFA = NF > 0 ? NF : 1;
+    constexpr int NT = 256, UB = 2;
+    if ((int)blockIdx.x >= *A.nrun) return;
+    const int b = A.list[blockIdx.x];
+    const ProbState st = A.st[b];
+    if (st.status != ST_RUNNING) return;
+    const int tid = threadIdx.x;
+    __shared__ double Bnd[4 * NJ];
+    if (tid < NJ) {
+        Bnd[tid] = C.q_lo[tid];
+        Bnd[NJ + tid] = C.q_hi[tid];
+        Bnd[2 * NJ + tid] = C.qd_lo[tid];
+        Bnd[3 * NJ + tid] = C.qd_hi[tid];
+    }
+    __syncthreads();
+    const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
+    const IpmSizes S = ipm_sizes(C);
+    const int N = C.N;
+    const double mu = st.mu, alpha = st.alpha, az = st.az, kappa_sigma = 1e10;
+    double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *Fv = A.F + b * S.f, *s = A.s + b * S.u;
+    double *yc = A.yc + b * S.u, *yl = A.yl + b * S.l, *yd = A.yd + b * S.u;
+    double *zqL = A.zqL + b * S.q, *zqU = A.zqU + b * S.q, *zdL = A.zdL + b * S.u, *zdU = A.zdU + b * S.u;
+    double *vL = A.vL + b * S.u, *vU = A.vU + b * S.u;
+    const double *dq = A.dq + b * S.q, *dqd = A.dqd + b * S.u, *dF = A.dF + b * S.f, *ds = A.ds + b * S.u;
+    const double *dyc = A.dyc + b * S.u, *dyl = A.dyl + b * S.l, *dyd = A.dyd + b * S.u;
+    const double *dzqL = A.dzqL + b * S.q, *dzqU = A.dzqU + b * S.q, *dzdL = A.dzdL + b * S.u, *dzdU = A.dzdU + b * S.u;
+    const double *dvL = A.dvL + b * S.u, *dvU = A.dvU + b * S.u;
+    const double *tlo = A.tau_lo, *thi = A.tau_hi;
     // ---------------- update (primal-dual step, then the bound multipliers with the new slacks)
     auto zupd = [&](double z, double dz, double slack) {
         const double zz = z + az * dz;
         return fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
     };
-    for (int e0 = lane; e0 < (N + 1) * n; e0 += 64 * UB) {
+    for (int e0 = tid; e0 < (N + 1) * n; e0 += NT * UB) {
         double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, (N + 1) * n - 1);
+            const int e = min(e0 + NT * u, (N + 1) * n - 1);
             x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; dzl[u] = dzqL[e]; zu[u] = zqU[e]; dzu[u] = dzqU[e];
         }
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
+            const int e = e0 + NT * u;
             if (e < (N + 1) * n) {
                 const int j = e % n;
                 const double xn = x[u] + alpha * dx[u];
@@ -1866,11 +2020,11 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
             }
         }
     }
-    for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
         double x[UB], xs[UB], zl[UB], zu[UB], vl[UB], vu[UB], lo[UB], hi[UB], yn[UB], dn[UB];
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + 64 * u, N * n - 1);
+            const int e = min(e0 + NT * u, N * n - 1);
             x[u] = qd[e] + alpha * dqd[e];
             xs[u] = s[e] + alpha * ds[e];
             yn[u] = yc[e] + alpha * dyc[e];
@@ -1884,7 +2038,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         };
 #pragma unroll
         for (int u = 0; u < UB; u++) {
-            const int e = e0 + 64 * u;
+            const int e = e0 + NT * u;
             if (e < N * n) {
                 const int k = e / n, j = e % n;
                 qd[e] = x[u]; s[e] = xs[u]; yc[e] = yn[u]; yd[e] = dn[u];
@@ -1897,20 +2051,9 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
             }
         }
     }
-    for (int e = lane; e < N * nf; e += 64) Fv[(e / nf) * NFA + e % nf] += alpha * dF[(e / nf) * NFA + e % nf];
-    for (int e = lane; e < N * nl; e += 64) yl[e] += alpha * dyl[e];
-    STAMP(6);
-    STAMP_COUNT(10, 1);
-    STAMP_FLUSH;
-    if (lane == 0) {
-        st.iter++;
-        st.mu = mu;
-        st.nu = nu;
-        A.st[b] = st;
-    }
-#undef TACT
+    for (int e = tid; e < N * nf; e += NT) Fv[(e / nf) * NFA + e % nf] += alpha * dF[(e / nf) * NFA + e % nf];
+    for (int e = tid; e < N * nl; e += NT) yl[e] += alpha * dyl[e];
 }
-
 
 // ============================================================== output in the reference layout
 template <int NJ, int NF>
@@ -2001,11 +2144,14 @@ struct IpmLaunch {
             hipLaunchKernelGGL((k_eval_asm<NJ, NF, NL>), dim3((unsigned)((nodes + NPBA - 1) / NPBA)), dim3(256), 0, s,
                                C, A, batch);
         } else if (phase == 2) {
-            hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, M, F, C, A, batch);
         } else if (phase == 3) {
+            hipLaunchKernelGGL((k_kkt_prep<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
             hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_kkt_recover<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
         } else {
             hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_post_update<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
             hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, A, batch);
         }
     }
