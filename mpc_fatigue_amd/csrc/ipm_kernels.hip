@@ -1406,10 +1406,11 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
     }
     constexpr int SLOT = MB * NJ + MB;       // Riccati slot (G_k | wv_k) doubles
     __shared__ double Hs[NVV];
-    __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], Pn[NJ * NJ];
+    __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], Pn[NJ * (NJ + 1)];
     __shared__ double Ks[NK * LDK], Rk[NK * NRK];
     __shared__ double Gl[NLA2 * NJ];
-    __shared__ double Ss5[(NU > 2 ? NU - 2 : 1) * (NU > 2 ? NU - 2 : 1)];  // reduced Hessian (stage_ns.hpp)
+    constexpr int NRS = NU > 2 ? NU - 2 : 1;
+    __shared__ double Ss5[NRS * NRS + 4 * NRS + 3];  // reduced Hessian + tables (stage_ns.hpp)
     __shared__ double Jl_s[NJ * NV];  // J_k (torque Jacobian) of the stage, regularised tries only
     // per-stage inputs of the recursion, computed for all stages at once by the whole wave (global
     // scratch, stage k contiguous): g_k (NV), c_k = q_k + h qd_k - q_{k+1} (NJ),
@@ -1439,6 +1440,7 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
             prep_dc = dc;
         }
         const bool dreg = (dw != 0.0 || dc != 0.0);
+        const bool dgreg = (dw != 0.0 || dFr != 0.0);  // diagonal regularisation of H
         // terminal value function V_N = 1/2 x^T P x + p^T x
         for (int e = lane; e < n * n; e += 64) {
             int i = e / n, j = e % n;
@@ -1488,7 +1490,7 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
                     if (dreg)
 #pragma unroll
                         for (int jj = 0; jj < NJ; jj++) a += Jl_s[jj * NV + u] * dDk[jj] * Jl_s[jj * NV + v];
-                    if (u == v) a += dw + (u >= 2 * n ? dFr : 0.0);
+                    if (dgreg && u == v) a += dw + (u >= 2 * n ? dFr : 0.0);
                     Hs[e] = a;
                 }
             }
@@ -1609,9 +1611,10 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
             }
             STAMP(14);
             // ---- P_k = Qxx + Qxu Ku + G^T Kl ; p_k = qx + Qxu ku + G^T kl   (block row a <-> control uo(a))
-            for (int e = lane; e < n * n; e += 64) {
-                int i = e / n, j = e % n;
-                double a = Hs[i * NV + j] + Ps[i * n + j];
+            // one pass over the n x (n + 1) entries [P_k | p_k] (column n of Rk holds ku, kl)
+            for (int e = lane; e < n * (n + 1); e += 64) {
+                const int i = e / (n + 1), j = e % (n + 1);
+                double a = (j < n) ? Hs[i * NV + j] + Ps[i * n + j] : gsk[i] + ss[i];
                 for (int r = 0; r < NU; r++) {
                     const int c = uo(r);
                     a += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[r * NRK + j];
@@ -1620,24 +1623,13 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
                     for (int l = 0; l < nl; l++) a += Gl[l * n + i] * Rk[(NU + l) * NRK + j];
                 Pn[e] = a;
             }
-            double pnew = 0.0;
-            if (lane < n) {
-                int i = lane;
-                pnew = gsk[i] + ss[i];
-                for (int r = 0; r < NU; r++) {
-                    const int c = uo(r);
-                    pnew += (Hs[i * NV + n + c] + (c < n ? h * Ps[i * n + c] : 0.0)) * Rk[r * NRK + n];
-                }
-                if (con)
-                    for (int l = 0; l < nl; l++) pnew += Gl[l * n + i] * Rk[(NU + l) * NRK + n];
-            }
             // (Ku, Kl, ku, kl stay in Rk: the next stage stores them, see the slot stores)
             wave_lds_sync();
             for (int e = lane; e < n * n; e += 64) {
                 int i = e / n, j = e % n;
-                Ps[e] = 0.5 * (Pn[e] + Pn[j * n + i]);
+                Ps[e] = 0.5 * (Pn[i * (n + 1) + j] + Pn[j * (n + 1) + i]);
             }
-            if (lane < n) ps[lane] = pnew;
+            if (lane < n) ps[lane] = Pn[lane * (n + 1) + n];
             wave_lds_sync();
             STAMP(15);
         }

@@ -15,7 +15,8 @@
 // so K has inertia (NU, 2) exactly when the reduced Hessian S = Z^T Q Z (NR x NR) is
 // positive definite, i.e. when its LDL^T without pivoting has positive pivots.  That is
 // the same exact test as the pivoted factorisation of K, with a fixed elimination order:
-//   * 25 lanes form S entry-wise from LDS reads of the stage Hessian and P (one round);
+//   * one lane per entry forms the lane-uniform tables Z_JR, Q_JR, Q_JJ in LDS, then 25 lanes form
+//     S entry-wise from them (the stage solve is FP64-issue bound: shared quantities are formed once);
 //   * every lane factors S redundantly in registers (no cross-lane traffic);
 //   * lane c solves right-hand side c:  u_p = D_J^{-1} b_l on J, u_R = S^{-1} Z^T (b_u - Q u_p),
 //     u_J = u_p,J + Z_JR u_R,  l = D_J^{-T} (b_u,J - (Q u)_J).
@@ -27,7 +28,18 @@
 
 namespace mf {
 
-// returns 1: solved, inertia (NU, 2); 0: wrong inertia; -1: degenerate (use the pivoted path)
+// 1/d to about one ulp: v_rcp_f64 and two Newton steps (a handful of FP64 instructions where a
+// correctly rounded division takes about ten; the stage solve is FP64-issue bound)
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+
+// returns 1: solved, inertia (NU, 2); 0: wrong inertia; -1: degenerate (use the pivoted path).
+// Ss5: LDS scratch of NR * NR + 4 * NR + 3 doubles (reduced Hessian, then the Z / Q tables).
 template <int NJ, int NF, int NV, int NRK>
 __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *Ps, const double *ss, const double *Gl,
                                                const double *gsk, const double *elk, double h, double *Ss5,
@@ -66,7 +78,8 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
     const int J0 = j1, J1 = j2;
     const double a00 = d0j1, a01 = h * Gl[J1], a10 = d1j1, a11 = h * Gl[NJ + J1];
     const double det = a00 * a11 - a01 * a10;
-    const double i00 = a11 / det, i01 = -a01 / det, i10 = -a10 / det, i11 = a00 / det;  // D_J^{-1}
+    const double rdet = 1.0 / det;
+    const double i00 = a11 * rdet, i01 = -a01 * rdet, i10 = -a10 * rdet, i11 = a00 * rdet;  // D_J^{-1}
     const int lo = J0 < J1 ? J0 : J1, hi = J0 < J1 ? J1 : J0;
     auto Ridx = [&](int m) {
         if (m >= NJ - 2) return NJ + (m - (NJ - 2));  // force controls
@@ -75,24 +88,32 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
         if (x >= hi) x++;
         return x;
     };
-    // Z_JR column m: -D_J^{-1} D[:, R_m]
-    auto Zc = [&](int m, double &z0, double &z1) {
+    // ---- lane-uniform tables, one entry per lane (every stage quantity the right-hand sides share is
+    // formed once, not per lane and per use): Z_JR = -D_J^{-1} D[:, R] (2 x NR), Q_JR (2 x NR),
+    // Q_JJ (q00, q01, q11).  Each lane evaluates both candidate forms and keeps its own.
+    double *Zt = Ss5 + NR * NR, *QJ = Zt + 2 * NR, *QJJ = QJ + 2 * NR;
+    if (lane < 4 * NR + 3) {
+        const int t = lane < 2 * NR ? lane : (lane < 4 * NR ? lane - 2 * NR : 0);
+        const int r = t / NR, m = t % NR;
         const int x = Ridx(m);
         const double e0 = Dc(0, x), e1 = Dc(1, x);
-        z0 = -(i00 * e0 + i01 * e1);
-        z1 = -(i10 * e0 + i11 * e1);
-    };
-    // ---- reduced Hessian S = Z^T Q Z, one entry per lane
+        const double zv = -((r == 0 ? i00 : i10) * e0 + (r == 0 ? i01 : i11) * e1);
+        // Q entry: (J_r, R_m) for the Q_JR lanes, (J0,J0), (J0,J1), (J1,J1) for the last three
+        const int u = lane - 4 * NR;
+        const int qa = lane < 4 * NR ? (r == 0 ? J0 : J1) : (u < 2 ? J0 : J1);
+        const int qb = lane < 4 * NR ? x : (u == 0 ? J0 : J1);
+        const double qv = Qe(qa, qb);
+        Ss5[NR * NR + lane] = lane < 2 * NR ? zv : qv;
+    }
+    wave_lds_sync();
+    const double q00 = QJJ[0], q01 = QJJ[1], q11 = QJJ[2];
+    // ---- reduced Hessian S = Z^T Q Z, one entry per lane (Q symmetric: Q_{R,J} = Q_{J,R})
     if (lane < NR * NR) {
         const int a = lane / NR, b = lane % NR;
-        const int Ra = Ridx(a), Rb = Ridx(b);
-        double za0, za1, zb0, zb1;
-        Zc(a, za0, za1);
-        Zc(b, zb0, zb1);
-        const double q00 = Qe(J0, J0), q01 = Qe(J0, J1), q11 = Qe(J1, J1);
-        double s = Qe(Ra, Rb);
-        s += za0 * Qe(J0, Rb) + za1 * Qe(J1, Rb);
-        s += Qe(Ra, J0) * zb0 + Qe(Ra, J1) * zb1;
+        const double za0 = Zt[a], za1 = Zt[NR + a], zb0 = Zt[b], zb1 = Zt[NR + b];
+        double s = Qe(Ridx(a), Ridx(b));
+        s += za0 * QJ[b] + za1 * QJ[NR + b];
+        s += QJ[a] * zb0 + QJ[NR + a] * zb1;
         s += za0 * (q00 * zb0 + q01 * zb1) + za1 * (q01 * zb0 + q11 * zb1);
         Ss5[lane] = s;
     }
@@ -107,7 +128,7 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
         for (int k = 0; k < j; k++) dj -= L[j][k] * L[j][k] * dg[k];
         dg[j] = dj;
         pd = pd && (dj > 0.0);
-        di[j] = 1.0 / dj;
+        di[j] = rcp_nr(dj);
 #pragma unroll
         for (int i = j + 1; i < NR; i++) {
             double v = Ss5[i * NR + j];
@@ -128,20 +149,13 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
         const double bl0 = c < NJ ? -Gl[c] : -elk[0];
         const double bl1 = c < NJ ? -Gl[NJ + c] : -elk[1];
         const double up0 = i00 * bl0 + i01 * bl1, up1 = i10 * bl0 + i11 * bl1;
-        const double q00 = Qe(J0, J0), q01 = Qe(J0, J1), q11 = Qe(J1, J1);
         const double bJ0 = bu(J0), bJ1 = bu(J1);
         const double rJ0 = bJ0 - q00 * up0 - q01 * up1;
         const double rJ1 = bJ1 - q01 * up0 - q11 * up1;
-        // Z_JR and Q_JR are re-read from LDS after the triangular solves rather than held through
-        // them (register budget of the whole Riccati kernel)
         double y[NR];
 #pragma unroll
-        for (int m = 0; m < NR; m++) {
-            const int x = Ridx(m);
-            double z0, z1;
-            Zc(m, z0, z1);
-            y[m] = bu(x) - Qe(J0, x) * up0 - Qe(J1, x) * up1 + z0 * rJ0 + z1 * rJ1;
-        }
+        for (int m = 0; m < NR; m++)
+            y[m] = bu(Ridx(m)) - QJ[m] * up0 - QJ[NR + m] * up1 + Zt[m] * rJ0 + Zt[NR + m] * rJ1;
 #pragma unroll
         for (int i = 0; i < NR; i++)
 #pragma unroll
@@ -155,13 +169,10 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
         double uJ0 = up0, uJ1 = up1, sJ0 = 0.0, sJ1 = 0.0;
 #pragma unroll
         for (int m = 0; m < NR; m++) {
-            const int x = Ridx(m);
-            double z0, z1;
-            Zc(m, z0, z1);
-            uJ0 += z0 * y[m];
-            uJ1 += z1 * y[m];
-            sJ0 += Qe(J0, x) * y[m];
-            sJ1 += Qe(J1, x) * y[m];
+            uJ0 += Zt[m] * y[m];
+            uJ1 += Zt[NR + m] * y[m];
+            sJ0 += QJ[m] * y[m];
+            sJ1 += QJ[NR + m] * y[m];
         }
         const double t0 = bJ0 - q00 * uJ0 - q01 * uJ1 - sJ0, t1 = bJ1 - q01 * uJ0 - q11 * uJ1 - sJ1;
         // D_J^T l = t  ->  l = D_J^{-T} t
