@@ -54,28 +54,30 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
         return v;
     };
     auto Dc = [&](int l, int x) { return x < NJ ? h * Gl[l * NJ + x] : 0.0; };
-    // ---- pivot columns of D (partial pivoting; ties keep the smallest index)
+    // ---- pivot columns of D (partial pivoting; ties keep the smallest index).  D = h Jl on the
+    // joint velocities: the pivot order depends on Jl alone (h > 0), and the second pivot compares
+    // |Jl1_j Jl0_j1 - Jl1_j1 Jl0_j| = |Jl0_j1| |(D_1j - f D_0j) / h| without the division by Jl0_j1.
     int j1 = 0;
-    double m1 = fabs(h * Gl[0]);
+    double m1 = fabs(Gl[0]);
 #pragma unroll
     for (int j = 1; j < NJ; j++) {
-        const double a = fabs(h * Gl[j]);
+        const double a = fabs(Gl[j]);
         if (a > m1) { m1 = a; j1 = j; }
     }
-    const double d0j1 = h * Gl[j1], d1j1 = h * Gl[NJ + j1];
+    const double g0 = Gl[j1], g1 = Gl[NJ + j1];
     int j2 = -1;
     double m2 = 0.0;
     if (m1 > 0.0) {
-        const double f = d1j1 / d0j1;
 #pragma unroll
         for (int j = 0; j < NJ; j++) {
             if (j == j1) continue;
-            const double a = fabs(h * Gl[NJ + j] - f * (h * Gl[j]));
+            const double a = fabs(Gl[NJ + j] * g0 - g1 * Gl[j]);
             if (a > m2) { m2 = a; j2 = j; }
         }
     }
-    if (!(m1 > 0.0) || j2 < 0 || !(m2 > 1e-10 * m1)) return -1;
+    if (!(m1 > 0.0) || j2 < 0 || !(m2 > 1e-10 * m1 * m1)) return -1;
     const int J0 = j1, J1 = j2;
+    const double d0j1 = h * g0, d1j1 = h * g1;
     const double a00 = d0j1, a01 = h * Gl[J1], a10 = d1j1, a11 = h * Gl[NJ + J1];
     const double det = a00 * a11 - a01 * a10;
     const double rdet = 1.0 / det;
@@ -119,21 +121,22 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
     }
     wave_lds_sync();
     // ---- LDL^T of S, redundantly in every lane (lower triangle of S is read)
-    double L[NR][NR], dg[NR], di[NR];
+    // LD[i][j] = L[i][j] d_j is the unscaled column entry itself: one FMA per update term
+    double L[NR][NR], LD[NR][NR], di[NR];
     bool pd = true;
 #pragma unroll
     for (int j = 0; j < NR; j++) {
         double dj = Ss5[j * NR + j];
 #pragma unroll
-        for (int k = 0; k < j; k++) dj -= L[j][k] * L[j][k] * dg[k];
-        dg[j] = dj;
+        for (int k = 0; k < j; k++) dj -= L[j][k] * LD[j][k];
         pd = pd && (dj > 0.0);
         di[j] = rcp_nr(dj);
 #pragma unroll
         for (int i = j + 1; i < NR; i++) {
             double v = Ss5[i * NR + j];
 #pragma unroll
-            for (int k = 0; k < j; k++) v -= L[i][k] * L[j][k] * dg[k];
+            for (int k = 0; k < j; k++) v -= L[i][k] * LD[j][k];
+            LD[i][j] = v;
             L[i][j] = v * di[j];
         }
     }
@@ -142,12 +145,14 @@ __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *P
     auto brow = [&](int x) { return x < NJ ? x + NF : x - NJ; };  // control -> block row of Rk
     if (lane < NRK) {
         const int c = lane;
-        auto bu = [&](int x) {
-            if (c < NJ) return -(Hs[(NJ + x) * NV + c] + (x < NJ ? h * Ps[x * NJ + c] : 0.0));
-            return -(gsk[NJ + x] + (x < NJ ? h * ss[x] : 0.0));
-        };
-        const double bl0 = c < NJ ? -Gl[c] : -elk[0];
-        const double bl1 = c < NJ ? -Gl[NJ + c] : -elk[1];
+        // right-hand side columns: -[Q_ux | q_u] (c < NJ: column c of Q_ux, c = NJ: q_u), the same
+        // instructions for every lane through per-lane base pointers and strides
+        const bool cq = c < NJ;
+        const double *hb = cq ? Hs + NJ * NV + c : gsk + NJ, *pb = cq ? Ps + c : ss, *gb = cq ? Gl + c : elk;
+        const int hst = cq ? NV : 1, pst = cq ? NJ : 1, gst = cq ? NJ : 1;
+        auto bu = [&](int x) { return -(hb[x * hst] + (x < NJ ? h * pb[x * pst] : 0.0)); };
+        const double bl0 = -gb[0];
+        const double bl1 = -gb[gst];
         const double up0 = i00 * bl0 + i01 * bl1, up1 = i10 * bl0 + i11 * bl1;
         const double bJ0 = bu(J0), bJ1 = bu(J1);
         const double rJ0 = bJ0 - q00 * up0 - q01 * up1;
