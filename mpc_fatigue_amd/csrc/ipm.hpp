@@ -15,6 +15,7 @@ struct ProbState {
     // (fraction to the boundary), grad(phi)^T dx and dx^T (W + Sigma) dx
     double ap, az, gdot, pHp;
     double alpha;          // accepted primal step (k_ipm_post -> k_post_update)
+    double phi0, th0;      // barrier objective and constraint violation at the iterate (k_kkt_recover -> k_ipm_post)
     int reg_tier;     // inertia correction of the last iteration: 0 none, 1 force block, 2 all primal
     int status;       // -1 running, 0 converged, 1 max_iter, 2 line-search failure, 3 inertia failure
     int iter, n_ls_fail, n_ic, consec_fail;

@@ -1112,7 +1112,7 @@ __global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, in
     if (st.status != ST_RUNNING) return;
     const int tid = threadIdx.x;
     __shared__ double Bnd[4 * NJ];
-    __shared__ double red[4 * (NT / 64)];
+    __shared__ double red[7 * (NT / 64)];
     if (tid < NJ) {
         Bnd[tid] = C.q_lo[tid];
         Bnd[NJ + tid] = C.q_hi[tid];
@@ -1133,8 +1133,9 @@ __global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, in
     double *dvL = A.dvL + b * S.u, *dvU = A.dvU + b * S.u;
     const double *tau = A.tau + b * S.u, *Jt = A.Jt + b * S.jt, *Jl = A.Jl + b * S.jl;
     const double *Ss = A.Ss + b * S.u, *gphs = A.gphs + b * S.u;
-    const double *W = A.W + b * S.w, *gf = A.gf + b * S.gf;
+    const double *W = A.W + b * S.w, *gf = A.gf + b * S.gf, *cost = A.cost + b * S.cost, *line = A.line + b * S.l;
     const double *Sxq = A.Sxq + b * S.q, *gphq = A.gphq + b * S.q, *gphd = A.gphd + b * S.u;
+    const double h = C.h;
     const double *G = A.G + b * S.G, *wv = A.wv + b * S.wv;
     const double *tlo = A.tau_lo, *thi = A.tau_hi;
     // fraction to the boundary (primal ap, bound multipliers az), accumulated where the steps are formed
@@ -1299,13 +1300,49 @@ __global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, in
         for (int u = 0; u < UB; u++)
             if (e0 + NT * u < N * n) { gdot += g1[u] + g2[u]; pHp += g3[u]; }
     }
-    double mx[2] = {-ap, -az}, sm[2] = {gdot, pHp};
-    block_reduce<NT, 2, 2>(mx, sm, red);
+    // merit terms at the iterate from the node evaluation of this iteration (the same values the
+    // line search's value sweep gives at alpha = 0, to round-off): objective, barrier, violation
+    double f0 = 0.0, bar0 = 0.0, th0 = 0.0;
+    for (int k = tid; k < N; k += NT) {
+        f0 += cost[k];
+        if (LINE_ON(k))
+#pragma unroll
+            for (int l = 0; l < NL; l++) th0 += fabs(line[k * nl + l]);
+    }
+    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
+        double xq[UB], xd[UB], xs[UB], tv[UB], qa[UB], lo[UB], hi[UB];
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = min(e0 + NT * u, N * n - 1);
+            xq[u] = q[e + n]; qa[u] = q[e]; xd[u] = qd[e]; xs[u] = s[e]; tv[u] = tau[e]; lo[u] = tlo[e]; hi[u] = thi[e];
+        }
+#pragma unroll
+        for (int u = 0; u < UB; u++) {
+            const int e = e0 + NT * u;
+            if (e < N * n) {
+                const int k = e / n, j = e % n;
+                if (hasb(lo[u]) || hasb(hi[u])) th0 += fabs(tv[u] - xs[u]);
+                th0 += fabs(qa[u] + h * xd[u] - xq[u]);
+                if (hasb(QLO[j])) bar0 -= log(xq[u] - QLO[j]);
+                if (hasb(QHI[j])) bar0 -= log(QHI[j] - xq[u]);
+                if (k > 0) {
+                    if (hasb(DLO[j])) bar0 -= log(xd[u] - DLO[j]);
+                    if (hasb(DHI[j])) bar0 -= log(DHI[j] - xd[u]);
+                }
+                if (hasb(lo[u])) bar0 -= log(xs[u] - lo[u]);
+                if (hasb(hi[u])) bar0 -= log(hi[u] - xs[u]);
+            }
+        }
+    }
+    double mx[2] = {-ap, -az}, sm[5] = {gdot, pHp, f0, bar0, th0};
+    block_reduce<NT, 2, 5>(mx, sm, red);
     if (tid == 0) {
         A.st[b].ap = -mx[0];
         A.st[b].az = -mx[1];
         A.st[b].gdot = sm[0];
         A.st[b].pHp = sm[1];
+        A.st[b].phi0 = sm[2] + mu * sm[3];
+        A.st[b].th0 = sm[4];
     }
 }
 
@@ -1897,13 +1934,9 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         theta = th;
         ok_out = (bad == 0);
     };
-    // merit at the current point through the same value sweep as the trial points, so that
-    // m(alpha) - m(0) carries no round-off mismatch between two code paths
-    double phi0, th0;
-    {
-        bool ok0;
-        merit(0.0, phi0, th0, ok0);
-    }
+    // merit at the current point from this iteration's node evaluation (k_kkt_recover); it equals the
+    // value sweep at alpha = 0 to round-off, which the acceptance test's 10 eps |m0| allowance covers
+    const double phi0 = st.phi0, th0 = st.th0;
     // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx (k_kkt_recover)
     const double gdot = st.gdot, pHp = st.pHp;
     if (th0 > 1e-300) {
