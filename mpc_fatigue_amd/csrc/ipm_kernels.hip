@@ -1302,7 +1302,10 @@ __global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, in
     }
     // merit terms at the iterate from the node evaluation of this iteration (the same values the
     // line search's value sweep gives at alpha = 0, to round-off): objective, barrier, violation
-    double f0 = 0.0, bar0 = 0.0, th0 = 0.0;
+    // the barrier term -sum log(gap) is taken as -log of the gaps' product, renormalised per element
+    // (mantissa pm, binary exponent pe): one log per thread instead of one per bound
+    double f0 = 0.0, bar0 = 0.0, th0 = 0.0, pm = 1.0;
+    int pe = 0, pe_ = 0;
     for (int k = tid; k < N; k += NT) {
         f0 += cost[k];
         if (LINE_ON(k))
@@ -1323,17 +1326,20 @@ __global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, in
                 const int k = e / n, j = e % n;
                 if (hasb(lo[u]) || hasb(hi[u])) th0 += fabs(tv[u] - xs[u]);
                 th0 += fabs(qa[u] + h * xd[u] - xq[u]);
-                if (hasb(QLO[j])) bar0 -= log(xq[u] - QLO[j]);
-                if (hasb(QHI[j])) bar0 -= log(QHI[j] - xq[u]);
+                if (hasb(QLO[j])) pm *= xq[u] - QLO[j];
+                if (hasb(QHI[j])) pm *= QHI[j] - xq[u];
                 if (k > 0) {
-                    if (hasb(DLO[j])) bar0 -= log(xd[u] - DLO[j]);
-                    if (hasb(DHI[j])) bar0 -= log(DHI[j] - xd[u]);
+                    if (hasb(DLO[j])) pm *= xd[u] - DLO[j];
+                    if (hasb(DHI[j])) pm *= DHI[j] - xd[u];
                 }
-                if (hasb(lo[u])) bar0 -= log(xs[u] - lo[u]);
-                if (hasb(hi[u])) bar0 -= log(hi[u] - xs[u]);
+                if (hasb(lo[u])) pm *= xs[u] - lo[u];
+                if (hasb(hi[u])) pm *= hi[u] - xs[u];
+                pm = frexp(pm, &pe_);
+                pe += pe_;
             }
         }
     }
+    bar0 = -(log(pm) + pe * 0.69314718055994530942);
     double mx[2] = {-ap, -az}, sm[5] = {gdot, pHp, f0, bar0, th0};
     block_reduce<NT, 2, 5>(mx, sm, red);
     if (tid == 0) {
@@ -1854,7 +1860,8 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
     // iterate and step are loaded into registers before the sweep starts.
     const int fpj = (NF > 0 || NL > 0) ? F.parent : -1;
     auto merit = [&](double alpha, double &phi, double &theta, bool &ok_out) {
-        double f = 0, bar = 0, th = 0;
+        double f = 0, bar = 0, th = 0, pm = 1.0;  // barrier: -log of the gaps' product, renormalised per element
+        int pe = 0, pe_ = 0;
         int bad = 0;
         for (int k = lane; k < N; k += 64) {
             // only the sweep's inputs are held through the sweep; slacks, bounds and q_{k+1} are
@@ -1917,17 +1924,20 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
                 const int e = e0 + 64 * u;
                 if (e < N * n) {
                     const int k = e / n, j = e % n;
-                    if (hasb(QLO[j])) { if (xq[u] - QLO[j] <= 0) bad = 1; else bar -= log(xq[u] - QLO[j]); }
-                    if (hasb(QHI[j])) { if (QHI[j] - xq[u] <= 0) bad = 1; else bar -= log(QHI[j] - xq[u]); }
+                    if (hasb(QLO[j])) { if (xq[u] - QLO[j] <= 0) bad = 1; else pm *= xq[u] - QLO[j]; }
+                    if (hasb(QHI[j])) { if (QHI[j] - xq[u] <= 0) bad = 1; else pm *= QHI[j] - xq[u]; }
                     if (k > 0) {
-                        if (hasb(DLO[j])) { if (xd[u] - DLO[j] <= 0) bad = 1; else bar -= log(xd[u] - DLO[j]); }
-                        if (hasb(DHI[j])) { if (DHI[j] - xd[u] <= 0) bad = 1; else bar -= log(DHI[j] - xd[u]); }
+                        if (hasb(DLO[j])) { if (xd[u] - DLO[j] <= 0) bad = 1; else pm *= xd[u] - DLO[j]; }
+                        if (hasb(DHI[j])) { if (DHI[j] - xd[u] <= 0) bad = 1; else pm *= DHI[j] - xd[u]; }
                     }
-                    if (hasb(lo[u])) { if (xs[u] - lo[u] <= 0) bad = 1; else bar -= log(xs[u] - lo[u]); }
-                    if (hasb(hi[u])) { if (hi[u] - xs[u] <= 0) bad = 1; else bar -= log(hi[u] - xs[u]); }
+                    if (hasb(lo[u])) { if (xs[u] - lo[u] <= 0) bad = 1; else pm *= xs[u] - lo[u]; }
+                    if (hasb(hi[u])) { if (hi[u] - xs[u] <= 0) bad = 1; else pm *= hi[u] - xs[u]; }
+                    pm = frexp(pm, &pe_);
+                    pe += pe_;
                 }
             }
         }
+        bar = -(log(pm) + pe * 0.69314718055994530942);
         f = wave_sum(f); bar = wave_sum(bar); th = wave_sum(th);
         bad = wave_sum_i(bad);
         phi = f + mu * bar;
