@@ -32,10 +32,12 @@ def load(fn, counter):
 def add_eval_phase(res, node_evals=None):
     """k_eval_node as the solver's phase 0: the q-class and qd-class launches of one iteration
     (one each per iteration), summed -- the unit bench.py's HIP-event timing uses."""
-    q, qd = res.get("k_eval_node[q]"), res.get("k_eval_node[qd]")
+    # the q directions run as k_eval_q (one wavefront per direction x 64 nodes) since 2ceaaeb
+    q, qd = res.get("k_eval_q") or res.get("k_eval_node[q]"), res.get("k_eval_node[qd]")
     if not q or not qd:
         return
-    ph = {"launches": q["launches"], "note": "phase = k_eval_node<..,0> + k_eval_node<..,1> (per-iteration sum)"}
+    ph = {"launches": q["launches"], "note": "phase = k_eval_q<..> (q directions) + k_eval_node<..,1> (qd directions), "
+          "per-iteration sum"}
     for f in ("read_bytes_per_launch", "write_bytes_per_launch", "hbm_bytes_per_launch", "fp64_flops_per_launch"):
         if f in q and f in qd:
             ph[f] = q[f] + qd[f]
