@@ -356,8 +356,15 @@ __global__ __launch_bounds__(64) void k_eval_q(const DevModel *__restrict__ Mg, 
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
     __shared__ double SCs[64][NJ][2], QDs[64][NJ], Cs[64][NJ], Ts[64][NJ];
-    const int v = (int)(blockIdx.x % NJ);
-    const long grp = blockIdx.x / NJ;
+    // XCD-aware block -> (node group, direction) map: workgroups are dealt round-robin over the 8 XCDs
+    // (blockIdx % 8), each with its own L2.  The NJ direction blocks of a node group write interleaved
+    // columns of the same W / Jt rows, so they are kept on one XCD (blockIdx % 8 = grp % 8) and issued
+    // back to back there: the rows' lines fill in one L2 instead of leaving it as NJ partial lines from
+    // NJ different L2s.  The grid is a multiple of 8 NJ blocks; blocks past the node groups exit.
+    const int xcd = (int)(blockIdx.x & 7);
+    const long slot = blockIdx.x >> 3;
+    const int v = (int)(slot % NJ);
+    const long grp = (slot / NJ) * 8 + xcd;
     const int lane = threadIdx.x;
     const int N = C.N;
     const long nslots = (long)*A.nrun * N;  // nodes of the compacted running set
@@ -2172,8 +2179,9 @@ struct IpmLaunch {
         long nodes = (long)nact * C.N;
         if (phase == 0) {
             const int nb = (int)((nodes + NPB - 1) / NPB);
-            hipLaunchKernelGGL((k_eval_q<NJ, NF, NL>), dim3((unsigned)(((nodes + 63) / 64) * NJ)), dim3(64), 0, s, M, F, C,
-                               A, batch);
+            const long ngrp8 = ((nodes + 63) / 64 + 7) / 8;  // node groups of 64, in rounds of 8 (one per XCD)
+            hipLaunchKernelGGL((k_eval_q<NJ, NF, NL>), dim3((unsigned)(ngrp8 * 8 * NJ)), dim3(64), 0, s, M, F, C, A,
+                               batch);
             hipLaunchKernelGGL((k_eval_node<NJ, NF, NL, 1>), dim3(nb), dim3(256), 0, s, M, F, C, A, batch, nb);
         } else if (phase == 1) {
             hipLaunchKernelGGL((k_eval_asm<NJ, NF, NL>), dim3((unsigned)((nodes + NPBA - 1) / NPBA)), dim3(256), 0, s,
