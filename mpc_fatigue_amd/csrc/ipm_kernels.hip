@@ -685,14 +685,21 @@ template <int NT> __device__ __forceinline__ double block_sum(double v, double *
     return sm[0];
 }
 
-template <int NJ, int NF, int NL>
-// One interior-point iteration = k_eval_node + three per-problem launches (one wave per
-// problem each; a launch boundary lets each phase have its own register budget):
-//   k_ipm_pre  : optimality error, convergence test, barrier update, barrier Sigma / gradients
-//   k_ipm_kkt  : inertia-corrected Riccati recursion, forward sweep, step recovery
-//   k_ipm_post : fraction to the boundary, merit line search, update
+// One interior-point iteration = the node evaluation (k_eval_q, k_eval_node<..,1>, k_eval_asm) + the
+// per-problem launches (a launch boundary lets each phase have its own register budget and block shape):
+//   k_ipm_pre     : optimality error, convergence test, barrier update, barrier Sigma / gradients, the
+//                   first inertia try's Riccati stage inputs (256-thread block per problem)
+//   k_ipm_kkt     : inertia-corrected Riccati recursion and forward sweep (one wave per problem)
+//   k_kkt_recover : step recovery, fraction to the boundary, merit slope / curvature (block per problem)
+//   k_ipm_post    : merit line search (one wave per problem); k_post_update: the update (block)
 // Scalars that cross a boundary travel in ProbState (mu, nu, tau_fb, regularisation, step bounds,
 // directional derivative and curvature).
+template <int NJ, int NF, int NL, int NT, class Sync>
+__device__ __forceinline__ void prep_stage_inputs(const OcpConst &C, const IpmArrays &A, int b, int tid, double dwv,
+                                                  double dcv, Sync sync);
+__device__ __forceinline__ void kkt_first_try(const ProbState &st, int &tier, double &reg, double &dw, double &dFr);
+
+template <int NJ, int NF, int NL>
 __global__ __launch_bounds__(256) void k_ipm_pre(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
     constexpr int n = NJ, nf = NF, nl = NL;
@@ -982,6 +989,15 @@ __global__ __launch_bounds__(256) void k_ipm_pre(const DevModel *__restrict__ Mg
         st.tau_fb = tau_fb;
         A.st[b] = st;
     }
+    // the first inertia try's per-stage inputs (Riccati stage blocks) from the Sigma and
+    // barrier gradients this block has just written (the __syncthreads above orders them): one launch
+    // and one re-read of those arrays per iteration less than a separate pass
+    {
+        int tier;
+        double reg, dw, dFr;
+        kkt_first_try(st, tier, reg, dw, dFr);
+        prep_stage_inputs<NJ, NF, NL, NT>(C, A, b, lane, dw, 0.0, [] { __syncthreads(); });
+    }
 #undef TACT
 }
 
@@ -990,7 +1006,7 @@ __global__ __launch_bounds__(256) void k_ipm_pre(const DevModel *__restrict__ Mg
 // Jl_{k+1} c_k, dD_k = D_tau(dw, dc) - Sigma_s (NJ), into stg (stage k contiguous, SG doubles), and
 // y_tau + D_tau r_tau (N x NJ) into the scratch behind it.  NT threads of one horizon (tid < NT)
 // stride the elements; `sync` orders the phases (a wave: s_waitcnt; a block: __syncthreads).
-// k_kkt_prep runs it for the first inertia try with a whole block per horizon; k_ipm_kkt reruns
+// k_ipm_pre runs it for the first inertia try with a whole block per horizon; k_ipm_kkt reruns
 // it in its own wave only when a retry changes (dw, dc).  Same per-element arithmetic either way.
 template <int NJ, int NF, int NL, int NT, class Sync>
 __device__ __forceinline__ void prep_stage_inputs(const OcpConst &C, const IpmArrays &A, int b, int tid, double dwv,
@@ -1079,27 +1095,13 @@ __device__ __forceinline__ void prep_stage_inputs(const OcpConst &C, const IpmAr
 }
 
 // Regularisation of an iteration's first inertia try (IPOPT's rule: a third of the last
-// successful perturbation, dropped below 1e-8; k_ipm_kkt and k_kkt_prep must agree on it).
+// successful perturbation, dropped below 1e-8; k_ipm_kkt and k_ipm_pre must agree on it).
 __device__ __forceinline__ void kkt_first_try(const ProbState &st, int &tier, double &reg, double &dw, double &dFr) {
     tier = st.reg_tier;
     reg = (st.reg_tier == 0) ? 0.0 : st.reg_last / 3.0;
     if (st.reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
     dw = (tier == 2) ? reg : 0.0;
     dFr = (tier == 1) ? reg : 0.0;
-}
-
-// The per-stage inputs of the first inertia try, one 256-thread block per running horizon: element
-// work that is latency-bound inside k_ipm_kkt's single wave runs here at full occupancy.
-template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(256) void k_kkt_prep(OcpConst C, IpmArrays A, int batch) {
-    if ((int)blockIdx.x >= *A.nrun) return;
-    const int b = A.list[blockIdx.x];
-    const ProbState st = A.st[b];
-    if (st.status != ST_RUNNING) return;
-    int tier;
-    double reg, dw, dFr;
-    kkt_first_try(st, tier, reg, dw, dFr);
-    prep_stage_inputs<NJ, NF, NL, 256>(C, A, b, threadIdx.x, dw, 0.0, [] { __syncthreads(); });
 }
 
 // Step recovery after k_ipm_kkt's sweeps, one 256-thread block per running horizon:
@@ -1480,7 +1482,7 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
     kkt_first_try(st, tier, reg, dw, dFr);
     bool factor_ok = false;
     int ntries = 0;
-    double prep_dw = dw, prep_dc = 0.0;  // k_kkt_prep wrote the first try's stage inputs
+    double prep_dw = dw, prep_dc = 0.0;  // k_ipm_pre wrote the first try's stage inputs
     for (int tries = 0; tries < 60; tries++) {
         ntries++;
         bool ok = true, zero = false;
@@ -2189,7 +2191,6 @@ struct IpmLaunch {
         } else if (phase == 2) {
             hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, M, F, C, A, batch);
         } else if (phase == 3) {
-            hipLaunchKernelGGL((k_kkt_prep<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
             hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
             hipLaunchKernelGGL((k_kkt_recover<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
         } else {

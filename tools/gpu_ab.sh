@@ -13,6 +13,6 @@ for R in 1 2; do
     python -c "import json; d=json.loads(open('$OUT/bench_${L}_$R.json').read().strip().splitlines()[-1]); k=d['roofline']['kernel_ms']; print('$L', round(d['value'],1), 'h/s', round(d['ms_per_step'],1), 'ms/step', 'iters', round(d['config']['mean_iters'],2), {a: round(b,1) for a,b in k.items()})"
   done
 done
-if [ -n "$PMC" ]; then bash tools/pmc_traffic.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -30 $OUT/pmc.log; exit 1; }
+if [ -n "$PMC" ]; then MF_LIB=${PMC_LIB:-libmpcfatigue.so} bash tools/pmc_traffic.sh $TAG/pmc > $OUT/pmc.log 2>&1 || { echo "pmc failed"; tail -30 $OUT/pmc.log; exit 1; }
   python -c "import json; d=json.load(open('$OUT/pmc/pmc_traffic.json')); print({k: (round(v['read_bytes_per_launch']/1e6,1), round(v['write_bytes_per_launch']/1e6,1)) for k,v in d.items() if isinstance(v,dict) and 'read_bytes_per_launch' in v})"
 fi
