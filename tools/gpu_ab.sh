@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
+MF_LIB=${TEST_LIB:-libmpcfatigue.so} timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 for R in 1 2; do
   for L in "$@"; do

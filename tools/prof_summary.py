@@ -20,14 +20,14 @@ def main(db_glob: str, out: str, title: str):
         ev = []
         for name, calls, tot, avg, pct in rows:
             short = name.split("(")[0].replace("void ", "")
-            if "k_eval_node<" in short:
+            if any(k in short for k in ("k_eval_node<", "k_eval_q<", "k_eval_dir<")):  # the direction classes
                 ev.append((calls, tot, avg, pct))
             if len(short) > 80:
                 short = short[:77] + "..."
             f.write(f"| `{short}` | {calls} | {tot:.1f} | {avg:.3f} | {pct:.2f} |\n")
         if len(ev) == 2:
             # the solver's phase 0 is one launch of each direction class per iteration
-            f.write(f"| **k_eval_node phase** (both classes) | {ev[0][0]} | {ev[0][1] + ev[1][1]:.1f} | "
+            f.write(f"| **k_eval_node phase** (q + qd direction launches) | {ev[0][0]} | {ev[0][1] + ev[1][1]:.1f} | "
                     f"{ev[0][2] + ev[1][2]:.3f} | {ev[0][3] + ev[1][3]:.2f} |\n")
     print(open(out).read())
 
