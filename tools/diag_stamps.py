@@ -30,7 +30,7 @@ res = ocp.solve(Q0, line_ref=LR, tol=1e-8, constr_viol_tol=1e-8, max_iter=300, F
 L = _lib.lib()
 buf = (C.c_ulonglong * (32 * B))()
 L.mf_debug_phase_stamps(buf, B)
-a = np.array(buf, dtype=np.float64).reshape(B, 32)
+a = np.array(buf, dtype=np.float64).reshape(B, 32)[:min(B, 4096)]  # the stamp buffer holds 4096 problems
 # KKT sub-phases (per stage, summed): 18 end of stage to loop top, 19 the wait for the prefetched
 # stage block, 7 H to LDS, 11 s=Pc+p + slot stores, 12 block assembly,
 # 13 Bunch-Kaufman factor, 14 solve, 15 P update; slot 2 keeps the rest of the KKT phase
@@ -47,3 +47,6 @@ for i, nm in enumerate(names):
     print(f"{nm:18s} {np.median(a[:, i] / it):12.0f} cyc/iter  {100 * a[:, i].sum() / tot.sum():5.1f}%")
 print("inertia tries / iter", np.mean(a_[:, 8] / it), " line-search trials / iter", np.mean(a_[:, 9] / it))
 print("stage factorisations / iter", np.mean(a_[:, 17] / it), " pivoted fallbacks / iter", np.mean(a_[:, 16] / it))
+stage = a_[:, [18, 19, 7, 11, 12, 13, 14, 15]].sum(1)
+print("Riccati stage loop: cycles per stage factorisation (median over problems):", np.median(stage / a_[:, 17]))
+
