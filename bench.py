@@ -152,6 +152,9 @@ def main() -> int:
     def solve_on(i):
         torch.cuda.set_device(dev)  # the HIP device is per host thread
         o, st, ob, pt = slots[i]
+        # N > 1: the RCCL gather of this slot's previous solutions was joined to the default stream;
+        # the new solve must not overwrite them before it has read them
+        st.wait_stream(torch.cuda.default_stream(dev))
         o.solve_dev(q0.data_ptr(), lref.data_ptr(), hi - lo, pt, stream=st.cuda_stream, **opts)
         st.synchronize()
 
