@@ -99,6 +99,11 @@ typedef struct {
     double mu_init;
     double F_init;         /* initial force guess (breaks the F = 0 saddle of -F^2) */
     int verbose;
+    int warm_start;        /* with a warm start w0: IPOPT warm_start_init_point = yes (RepeatedMPCwithThermal.py:
+                              445-446, mpc_principal.py:349-351) -- warm_start_bound_push = _frac = 1e-3 for the
+                              primal point and the slacks, bound multipliers warm_start_mult_bound_push = 1e-3
+                              (CasADi passes lam_x0 = 0), constraint multipliers 0 (lam_g0 = 0); 0: cold
+                              constants (bound_push = bound_frac = 1e-2, bound multipliers 1) */
 } mf_solver_opts;
 
 int mf_problem_create(const mf_model *m, const mf_problem_spec *spec, mf_problem **out);
@@ -142,7 +147,7 @@ int mf_ik_batch_dev(const mf_model *m, int frame, const double *target, const do
  * RepeatedMPCwithThermal.py:445-487: Solver(x0 = sol, ...) with ipopt warm_start_init_point):
  * qd0 (batch x n, or NULL = the spec's) is each problem's fixed qd_0; w0 (batch x wsize, or NULL
  * = cold start) supplies q_k, qd_k (k >= 1) and F_k, pushed into their bounds; q_0 is q0.
- * Multipliers start cold.  w0 must not alias w. */
+ * Multipliers start at IPOPT's cold (opts->warm_start = 0) or warm-start values.  w0 must not alias w. */
 int mf_solve_batch_ws(mf_problem *p, int batch, const double *q0, const double *qd0, const double *w0,
                       const double *line_ref, const mf_solver_opts *opts, double *w, int *status, int *iters,
                       double *kkt, double *obj, int device);
@@ -224,6 +229,7 @@ typedef struct {
     const double *u_init;  /* nu initial controls used at every node (host memory), or NULL */
     int max_soc;           /* second-order corrections per iteration (IPOPT max_soc; 0 = off) */
     int verbose;
+    int warm_start;        /* as mf_solver_opts.warm_start (IPOPT warm_start_init_point with w0) */
 } mf_gopts;
 
 int mf_gproblem_create(const mf_model *m0, const mf_model *m1, const mf_gspec *spec, mf_gproblem **out);

@@ -73,12 +73,13 @@ class GOpts(C.Structure):
     """mf_gopts (include/mpcfatigue.h)."""
     _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
                 ("mu_init", C.c_double), ("init_zero", C.c_int), ("F_init", C.c_double),
-                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("verbose", C.c_int)]
+                ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("verbose", C.c_int),
+                ("warm_start", C.c_int)]
 
 
 class SolverOpts(C.Structure):
     _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
-                ("mu_init", C.c_double), ("F_init", C.c_double), ("verbose", C.c_int)]
+                ("mu_init", C.c_double), ("F_init", C.c_double), ("verbose", C.c_int), ("warm_start", C.c_int)]
 
 
 _lib = None

@@ -587,6 +587,7 @@ static int solve_core(mf_problem *p, int batch, const double *d_q0, const double
     C.max_iter = o ? o->max_iter : 200;
     C.mu_init = o ? o->mu_init : 0.1;
     C.F_init = o ? o->F_init : 0.0;
+    C.warm_start = (o && d_w0) ? o->warm_start : 0;
     IpmArrays A = p->A;
     A.qd0p = d_qd0;
     A.w0 = d_w0;

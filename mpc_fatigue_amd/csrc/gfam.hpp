@@ -55,6 +55,7 @@ struct GParams {
     // solver options
     double tol, constr_viol_tol, mu_init, F_init;
     int max_iter, max_soc, init_zero, has_u_init;
+    int warm_start, pad_ws;  // IPOPT warm_start_init_point constants for a w0 start (k_ginit)
     double u_init[GX_MAX];
     int force_from, tier1_from, tier1_to;  // first force control; u range regularised first (concave cost)
     int target_decimals;                   // CentauroFam: round the relative-pose targets (-1: exact)

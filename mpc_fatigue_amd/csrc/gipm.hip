@@ -71,8 +71,9 @@ template <class D> struct GSz {
 
 __device__ __forceinline__ bool gb(double b) { return isfinite(b); }
 
-__device__ __forceinline__ double gpush(double x, double lo, double hi) {
-    const double k1 = 1e-2, k2 = 1e-2;
+// IPOPT bound_push = bound_frac (k1 = k2): 1e-2 cold, warm_start_bound_push = _frac = 1e-3 warm
+__device__ __forceinline__ double gpush(double x, double lo, double hi, double k1 = 1e-2) {
+    const double k2 = k1;
     const bool hl = gb(lo), hh = gb(hi);
     if (hl && hh) {
         const double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
@@ -195,13 +196,18 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
     }
     const int wst = NU + NX, wsz = NX + N * wst;
     const double *w0 = A.w0 ? A.w0 + (size_t)b * wsz : nullptr;
+    // IPOPT initial point: bound_push = bound_frac = 1e-2 and bound multipliers 1 (bound_mult_init_val);
+    // warm_start_init_point: 1e-3 and warm_start_mult_bound_push = 1e-3 (oracle/mf_ocp.c, same rule)
+    const bool warm = P.warm_start && w0;
+    const double kp = warm ? 1e-3 : 1e-2, z0 = warm ? 1e-3 : 1.0;
     for (int e = lane; e < (N + 1) * NX; e += 64) {
         const int k = e / NX, j = e % NX;
         double v = x0[j];
-        if (k > 0) v = gpush(w0 ? w0[NX + (k - 1) * wst + NU + j] : (P.init_zero ? 0.0 : x0[j]), P.x_lo[j], P.x_hi[j]);
+        if (k > 0)
+            v = gpush(w0 ? w0[NX + (k - 1) * wst + NU + j] : (P.init_zero ? 0.0 : x0[j]), P.x_lo[j], P.x_hi[j], kp);
         x[e] = v;
-        A.zxL[b * Z.x() + e] = (k > 0 && gb(P.x_lo[j])) ? 1.0 : 0.0;
-        A.zxU[b * Z.x() + e] = (k > 0 && gb(P.x_hi[j])) ? 1.0 : 0.0;
+        A.zxL[b * Z.x() + e] = (k > 0 && gb(P.x_lo[j])) ? z0 : 0.0;
+        A.zxU[b * Z.x() + e] = (k > 0 && gb(P.x_hi[j])) ? z0 : 0.0;
     }
     for (int e = lane; e < N * NU; e += 64) {
         const int k = e / NU, j = e % NU;
@@ -213,11 +219,11 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         } else {
             double v0 = P.has_u_init ? P.u_init[j] : (j >= P.force_from ? P.F_init : 0.0);
             if (w0) v0 = w0[NX + k * wst + j];
-            v = gpush(v0, lo, hi);
+            v = gpush(v0, lo, hi, kp);
         }
         u[e] = v;
-        A.zuL[b * Z.u() + e] = (!fixed && gb(lo)) ? 1.0 : 0.0;
-        A.zuU[b * Z.u() + e] = (!fixed && gb(hi)) ? 1.0 : 0.0;
+        A.zuL[b * Z.u() + e] = (!fixed && gb(lo)) ? z0 : 0.0;
+        A.zuU[b * Z.u() + e] = (!fixed && gb(hi)) ? z0 : 0.0;
     }
     for (int e = lane; e < N * NX; e += 64) A.lam[b * Z.l() + e] = 0.0;
     for (int e = lane; e < N * NET; e += 64) A.ye[b * Z.e() + e] = 0.0;
@@ -229,9 +235,9 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         for (int r = 0; r < NI; r++) {
             const int i = k * NIA + r;
             const double lo = A.c_lo[k * NI + r], hi = A.c_hi[k * NI + r];
-            s[i] = gpush(ci[r], lo, hi);
-            A.vL[b * Z.i() + i] = gb(lo) ? 1.0 : 0.0;
-            A.vU[b * Z.i() + i] = gb(hi) ? 1.0 : 0.0;
+            s[i] = gpush(ci[r], lo, hi, kp);
+            A.vL[b * Z.i() + i] = gb(lo) ? z0 : 0.0;
+            A.vU[b * Z.i() + i] = gb(hi) ? z0 : 0.0;
         }
     }
     if (lane == 0) {
@@ -1146,6 +1152,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     P.init_zero = o ? o->init_zero : 0;
     P.F_init = o ? o->F_init : 0.0;
     P.max_soc = o ? o->max_soc : 4;
+    P.warm_start = (o && d_w0) ? o->warm_start : 0;
     P.has_u_init = (o && o->u_init) ? 1 : 0;
     if (P.has_u_init)
         for (int j = 0; j < D::NU; j++) P.u_init[j] = o->u_init[j];

@@ -35,6 +35,7 @@ struct OcpConst {
     // solver options
     double tol, constr_viol_tol, mu_init, F_init;
     int max_iter;
+    int warm_start;        // IPOPT warm_start_init_point constants for a w0 start (k_ipm_init)
 };
 
 // Device arrays; every per-problem array is [batch][size] with the size below.

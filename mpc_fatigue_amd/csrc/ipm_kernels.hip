@@ -65,9 +65,10 @@ __device__ unsigned long long mf_stamp_buf[32 * 4096];
 #define STAMP_FLUSH do {} while (0)
 #endif
 
-// IPOPT bound_push / bound_frac = 1e-2: move an initial value strictly inside its bounds
-__device__ __forceinline__ double bound_push(double x, double lo, double hi) {
-    const double k1 = 1e-2, k2 = 1e-2;
+// IPOPT bound_push / bound_frac = 1e-2 (warm_start_bound_push / _frac = 1e-3 for a warm start): move an
+// initial value strictly inside its bounds
+__device__ __forceinline__ double bound_push(double x, double lo, double hi, double k1 = 1e-2) {
+    const double k2 = k1;
     bool hl = hasb(lo), hh = hasb(hi);
     if (hl && hh) {
         double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
@@ -554,30 +555,33 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
     const int N = C.N;
     double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *Fv = A.F + b * S.f, *s = A.s + b * S.u;
     const double *q0 = A.q0 + (size_t)b * NJ;
+    // warm start (w layout [q_0 | (qd_k, F_k, q_{k+1}) for k < N]): q_k, qd_k (k >= 1) and F_k from w0,
+    // pushed into their bounds; q_0, qd_0 stay this problem's.  IPOPT warm_start_init_point (C.warm_start):
+    // pushes 1e-3 instead of 1e-2 and bound multipliers 1e-3 instead of 1 (oracle/mf_oracle.c, same rule)
+    const int wst = 2 * NJ + NF, wsz = NJ + N * wst;
+    const double *w0 = A.w0 ? A.w0 + (size_t)b * wsz : nullptr;
+    const bool warm = C.warm_start && w0;
+    const double kp = warm ? 1e-3 : 1e-2, z0 = warm ? 1e-3 : 1.0;
     for (int e = lane; e < (N + 1) * NJ; e += 64) {
         int k = e / NJ, j = e % NJ;
         q[e] = (k == 0) ? q0[j] : bound_push(q0[j], C.q_lo[j], C.q_hi[j]);
-        A.zqL[b * S.q + e] = (k > 0 && hasb(C.q_lo[j])) ? 1.0 : 0.0;
-        A.zqU[b * S.q + e] = (k > 0 && hasb(C.q_hi[j])) ? 1.0 : 0.0;
+        A.zqL[b * S.q + e] = (k > 0 && hasb(C.q_lo[j])) ? z0 : 0.0;
+        A.zqU[b * S.q + e] = (k > 0 && hasb(C.q_hi[j])) ? z0 : 0.0;
     }
-    // warm start (w layout [q_0 | (qd_k, F_k, q_{k+1}) for k < N]): q_k, qd_k (k >= 1) and F_k from w0,
-    // pushed into their bounds; q_0, qd_0 stay this problem's
-    const int wst = 2 * NJ + NF, wsz = NJ + N * wst;
-    const double *w0 = A.w0 ? A.w0 + (size_t)b * wsz : nullptr;
     if (w0) {
         for (int e = lane + NJ; e < (N + 1) * NJ; e += 64) {
             const int k = e / NJ, j = e % NJ;
-            q[e] = bound_push(w0[NJ + (k - 1) * wst + NJ + NF + j], C.q_lo[j], C.q_hi[j]);
+            q[e] = bound_push(w0[NJ + (k - 1) * wst + NJ + NF + j], C.q_lo[j], C.q_hi[j], kp);
         }
     }
     for (int e = lane; e < N * NJ; e += 64) {
         int k = e / NJ, j = e % NJ;
         const double qd0j = A.qd0p ? A.qd0p[(size_t)b * NJ + j] : C.qd0[j];
-        qd[e] = (k == 0) ? qd0j : bound_push(w0 ? w0[NJ + k * wst + j] : 0.0, C.qd_lo[j], C.qd_hi[j]);
-        A.zdL[b * S.u + e] = (k > 0 && hasb(C.qd_lo[j])) ? 1.0 : 0.0;
-        A.zdU[b * S.u + e] = (k > 0 && hasb(C.qd_hi[j])) ? 1.0 : 0.0;
-        A.vL[b * S.u + e] = hasb(A.tau_lo[e]) ? 1.0 : 0.0;
-        A.vU[b * S.u + e] = hasb(A.tau_hi[e]) ? 1.0 : 0.0;
+        qd[e] = (k == 0) ? qd0j : bound_push(w0 ? w0[NJ + k * wst + j] : 0.0, C.qd_lo[j], C.qd_hi[j], kp);
+        A.zdL[b * S.u + e] = (k > 0 && hasb(C.qd_lo[j])) ? z0 : 0.0;
+        A.zdU[b * S.u + e] = (k > 0 && hasb(C.qd_hi[j])) ? z0 : 0.0;
+        A.vL[b * S.u + e] = hasb(A.tau_lo[e]) ? z0 : 0.0;
+        A.vU[b * S.u + e] = hasb(A.tau_hi[e]) ? z0 : 0.0;
         A.yc[b * S.u + e] = 0.0;
         A.yd[b * S.u + e] = 0.0;
     }
@@ -589,9 +593,10 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
     struct SlackOut {
         double *s;
         const double *lo, *hi;
+        double kp;
         __device__ void frame(const double *) {}
         __device__ void force(const double *) {}
-        __device__ void joint(int j, double t, double, double) { s[j] = bound_push(t, lo[j], hi[j]); }
+        __device__ void joint(int j, double t, double, double) { s[j] = bound_push(t, lo[j], hi[j], kp); }
     };
     const int fp = (NF > 0 || NL > 0) ? F.parent : -1;
     for (int k = lane; k < N; k += 64) {
@@ -604,7 +609,7 @@ __global__ __launch_bounds__(64) void k_ipm_init(const DevModel *__restrict__ Mg
             Fw[r] = acc;
         }
         ArrIn<NJ> in{q + (size_t)k * NJ, qd + (size_t)k * NJ};
-        SlackOut so{s + (size_t)k * NJ, A.tau_lo + (size_t)k * NJ, A.tau_hi + (size_t)k * NJ};
+        SlackOut so{s + (size_t)k * NJ, A.tau_lo + (size_t)k * NJ, A.tau_hi + (size_t)k * NJ, kp};
         node_values<NJ>(M, F, fp, in, Fw, so);
     }
     if (lane == 0) {

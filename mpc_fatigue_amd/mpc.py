@@ -7,8 +7,10 @@ the previous solution (``python/Centauro_script/mpc_principal.py:357-377``,
 * ``q0 <- sol[N*n : N*n + nq]``   -- the joint angles at the last node (q_N),
 * ``qc_dot0 <- sol[k*n + 2nq : ...]`` with the loop variable left at k = N-1 -- the last
   joint velocity (qd_{N-1}),
-* ``Solver(x0 = sol, ...)`` with IPOPT ``warm_start_init_point``: the previous primal point,
-  multipliers cold.
+* ``Solver(x0 = sol, ...)`` with IPOPT ``warm_start_init_point = yes`` (``RepeatedMPCwithThermal.py:445-446``
+  from the second solve on): the previous primal point pushed into its bounds by
+  warm_start_bound_push = _frac = 1e-3, bound multipliers warm_start_mult_bound_push = 1e-3 (CasADi
+  passes lam_x0 = 0), constraint multipliers 0 (lam_g0 = 0); mu_init stays IPOPT's 0.1.
 
 ``RecedingHorizon`` runs that loop for a batch of horizons through ``mf_solve_batch_ws``
 (the GPU init kernel pushes the warm start into the bounds exactly as the oracle does).
@@ -49,16 +51,29 @@ def next_initial_state(w: np.ndarray, n: int, nf: int, N: int):
 class RecedingHorizon:
     """Repeated OCP solves of the spec's problem for a batch of initial states."""
 
-    def __init__(self, spec: dict, carry_velocity: bool = True, **opts):
+    def __init__(self, spec: dict, carry_velocity: bool = True, warm_start: bool = True,
+                 reanchor_line: bool = False, **opts):
         """carry_velocity: restart with qd_0 = qd_{N-1} as the reference does.  For the C2 line
         task that velocity sits on its +-0.4 bounds at the end of a horizon, and the next
-        horizon is then infeasible (the frame cannot return to the line by node 2; the oracle
-        and the GPU both stop at max_iter with the same violation), so the C2 loop restarts
-        at rest (carry_velocity=False)."""
+        horizon is then often infeasible (the frame cannot return to the line by node 2: 18 of
+        96 restarts fail even from a cold start), so the C2 loop restarts at rest
+        (carry_velocity=False).
+        warm_start: IPOPT warm_start_init_point constants for the solves after the first.
+        reanchor_line: each horizon's line reference is the frame position of its own q_0 (as
+        the C5 batch anchors every horizon, problems.pilz6_batch_q0).  The transcription puts the
+        line on nodes k < N only (force_optimization_pilz_6DOF.py:150-156 inside ``for k in
+        range(N)``), so q_N may end off a fixed line and the restarted horizon then has to reach it
+        by node 2 with |qd| <= 0.4: at the edge of that reach the line rows and the active velocity
+        bounds are linearly dependent and the multipliers diverge (measured: DESIGN.md s.3)."""
         self.spec = spec
         self.ocp = OCP(spec)
         self.carry_velocity = carry_velocity
+        self.warm_start = warm_start
+        self.reanchor_line = reanchor_line
         self.opts = opts
+        if reanchor_line:
+            from .pin import ForwardKinematics
+            self._fk = ForwardKinematics(self.ocp.model, spec["frame"])
 
     def run(self, q0, steps: int, line_ref=None, qd0=None):
         """Returns the list of per-step SolveResults (host arrays)."""
@@ -67,7 +82,10 @@ class RecedingHorizon:
         qd = None if qd0 is None else np.atleast_2d(np.asarray(qd0, float))
         w0, out = None, []
         for _ in range(steps):
-            r = o.solve_ws(q0, qd0=qd, w0=w0, line_ref=line_ref, **self.opts)
+            if self.reanchor_line:
+                line_ref = self._fk.batch(q0)[0][:, :2]
+            r = o.solve_ws(q0, qd0=qd, w0=w0, line_ref=line_ref,
+                           warm_start=self.warm_start and w0 is not None, **self.opts)
             out.append(r)
             q0, qdl = next_initial_state(r.w, o.n, o.nf, o.N)
             qd = qdl if self.carry_velocity else None
@@ -103,9 +121,10 @@ class GRecedingHorizon:
     as mpc_principal.py:357-377 restarts the Centauro MPC."""
 
     def __init__(self, spec: dict, carry_velocity: bool = True, T_drop: float = 0.05, decimals: int | None = 4,
-                 models=None, restart_spec: dict | None = None, **opts):
+                 models=None, restart_spec: dict | None = None, warm_start: bool = True, **opts):
         """restart_spec: the problem solved from the second step on (the Centauro loop rounds its
-        relative-pose targets after the first solve, RepeatedMPCwithThermal.py:485-486); default spec."""
+        relative-pose targets after the first solve, RepeatedMPCwithThermal.py:485-486); default spec.
+        warm_start: IPOPT warm_start_init_point constants from the second solve on (L445-446)."""
         self.spec = spec
         self.g = GOCP(spec, models=models)
         self.g_restart = GOCP(restart_spec, models=self.g.models) if restart_spec is not None else self.g
@@ -114,6 +133,7 @@ class GRecedingHorizon:
         self.carry_velocity = carry_velocity
         self.T_drop = T_drop
         self.decimals = decimals
+        self.warm_start = warm_start
         self.opts = opts
 
     def next_initial(self, w):
@@ -146,7 +166,8 @@ class GRecedingHorizon:
             ptr["w"] = w.data_ptr()
             (g if s == 0 else self.g_restart).solve_dev(
                 x.data_ptr(), None if u is None else u.data_ptr(), None if prev is None else prev.data_ptr(),
-                None if lr is None else lr.data_ptr(), B, ptr, stream=stream, **self.opts)
+                None if lr is None else lr.data_ptr(), B, ptr, stream=stream,
+                warm_start=self.warm_start and prev is not None, **self.opts)
             res.append(SolveResult(w.cpu().numpy(), out["status"].cpu().numpy(), out["iters"].cpu().numpy(),
                                    out["kkt"].cpu().numpy(), out["obj"].cpu().numpy()))
             x, u = self.next_initial(w)

@@ -34,8 +34,10 @@ class SolveResult:
         return self.status == 0
 
 
-def default_opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=200, mu_init=0.1, F_init=0.0, verbose=False):
-    return _lib.SolverOpts(tol, constr_viol_tol, max_iter, mu_init, F_init, int(verbose))
+def default_opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=200, mu_init=0.1, F_init=0.0, verbose=False,
+                 warm_start=False):
+    """mf_solver_opts; warm_start: IPOPT warm_start_init_point constants for a w0 start."""
+    return _lib.SolverOpts(tol, constr_viol_tol, max_iter, mu_init, F_init, int(verbose), int(warm_start))
 
 
 class OCP:

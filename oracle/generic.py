@@ -56,7 +56,8 @@ class GOpts(C.Structure):
                 ("mu_init", C.c_double), ("init_zero", C.c_int), ("verbose", C.c_int), ("F_init", C.c_double),
                 ("w0", C.POINTER(C.c_double)), ("bound_relax", C.c_double),
                 ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("dual_out", C.POINTER(C.c_double)),
-                ("node_cb", C.c_void_p), ("node_ctx", C.c_void_p), ("val_cb", C.c_void_p)]
+                ("node_cb", C.c_void_p), ("node_ctx", C.c_void_p), ("val_cb", C.c_void_p),
+                ("warm_start", C.c_int), ("dual_in", C.POINTER(C.c_double))]
 
 
 _lib = None
@@ -220,9 +221,13 @@ def w_size(g: GOCP) -> int:
 
 
 def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, verbose=0, F_init=0.0,
-         w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None, node_cb=None, node_ctx=None, val_cb=None):
+         w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None, node_cb=None, node_ctx=None, val_cb=None,
+         warm_start=False, dual_in=None):
     o = GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), F_init, None, bound_relax, None,
-              max_soc, None, node_cb, node_ctx, val_cb)
+              max_soc, None, node_cb, node_ctx, val_cb, int(warm_start), None)
+    if dual_in is not None:
+        o._di = np.ascontiguousarray(dual_in, dtype=np.float64)
+        o.dual_in = _p(o._di)
     if dual_out is not None:
         o._d = dual_out
         o.dual_out = _p(dual_out)

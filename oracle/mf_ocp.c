@@ -98,6 +98,12 @@ typedef struct {
     /* optional value provider of the same library (l, c_in, c_eq, f at one node); NULL = hyper-dual */
     int (*val_cb)(void *ctx, const double *x, const double *u, const double *lref, double *l, double *ci,
                   double *ce, double *f);
+    /* IPOPT warm_start_init_point = yes (RepeatedMPCwithThermal.py:445-446, mpc_principal.py:349-351): the
+     * primal point of w0 pushed by warm_start_bound_push / _frac = 1e-3 (slacks: warm_start_slack_bound_*
+     * = 1e-3), bound multipliers max(given, warm_start_mult_bound_push = 1e-3), constraint multipliers as
+     * given (CasADi's lam_g0 defaults to 0).  dual_in: optional multipliers in the dual_out layout. */
+    int warm_start;
+    const double *dual_in;
 } mfg_opts;
 
 typedef struct {
@@ -406,8 +412,8 @@ static void eval_derivs(ws_t *S, int k) {
         }
 }
 
-static double push_into(double x, double lo, double hi) {
-    const double k1 = 1e-2, k2 = 1e-2;
+/* IPOPT bound_push / bound_frac (1e-2 cold; warm_start_bound_push / _frac = 1e-3 warm) */
+static double push_into_k(double x, double lo, double hi, double k1, double k2) {
     int hl = hasb(lo), hh = hasb(hi);
     if (hl && hh) {
         double pl = fmin(k1 * fmax(1.0, fabs(lo)), k2 * (hi - lo));
@@ -421,6 +427,7 @@ static double push_into(double x, double lo, double hi) {
     }
     return x;
 }
+static double push_into(double x, double lo, double hi) { return push_into_k(x, lo, hi, 1e-2, 1e-2); }
 
 /* barrier objective and l1 constraint violation at (x, u, s); optionally the residual vectors */
 static void merit_parts(const ws_t *S, const double *x, const double *u, const double *s, double mu, double *phi,
@@ -891,34 +898,51 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
             double v = O->u_init ? O->u_init[j] : ((j >= P->force_from) ? O->F_init : 0.0);
             S->u[i] = S->ufix[i] ? S->ulo[i] : push_into(v, S->ulo[i], S->uhi[i]);
         }
+    const int warm = O->warm_start && O->w0;
+    const double kp = warm ? 1e-3 : 1e-2;  /* (warm_start_)bound_push = _frac */
     if (O->w0) {
         const int st = nu + nx;
         for (int k = 0; k < N; k++) {
             const double *wk = O->w0 + nx + (size_t)k * st;
             for (int j = 0; j < nu; j++) {
                 const int i = k * nu + j;
-                if (!S->ufix[i]) S->u[i] = push_into(wk[j], S->ulo[i], S->uhi[i]);
+                if (!S->ufix[i]) S->u[i] = push_into_k(wk[j], S->ulo[i], S->uhi[i], kp, kp);
             }
-            for (int j = 0; j < nx; j++) S->x[(k + 1) * nx + j] = push_into(wk[nu + j], S->xlo[j], S->xhi[j]);
+            for (int j = 0; j < nx; j++)
+                S->x[(k + 1) * nx + j] = push_into_k(wk[nu + j], S->xlo[j], S->xhi[j], kp, kp);
         }
     }
     for (int k = 0; k < N; k++) {
         double l, ci[GI], ce[GE], f[GX];
         eval_values(S, k, S->x + k * nx, S->u + k * nu, &l, ci, ce, f);
-        for (int r = 0; r < ni; r++) S->s[k * ni + r] = push_into(ci[r], S->clo[k * ni + r], S->chi[k * ni + r]);
+        for (int r = 0; r < ni; r++)
+            S->s[k * ni + r] = push_into_k(ci[r], S->clo[k * ni + r], S->chi[k * ni + r], kp, kp);
     }
+    /* bound multipliers: bound_mult_init_val = 1 cold; warm: max(given (0 when none),
+     * warm_start_mult_bound_push = 1e-3) */
+    const double z0 = warm ? 1e-3 : 1.0;
     for (int k = 0; k <= N; k++)
         for (int j = 0; j < nx; j++) {
-            S->zxL[k * nx + j] = (k > 0 && hasb(S->xlo[j])) ? 1.0 : 0.0;
-            S->zxU[k * nx + j] = (k > 0 && hasb(S->xhi[j])) ? 1.0 : 0.0;
+            S->zxL[k * nx + j] = (k > 0 && hasb(S->xlo[j])) ? z0 : 0.0;
+            S->zxU[k * nx + j] = (k > 0 && hasb(S->xhi[j])) ? z0 : 0.0;
         }
     for (int i = 0; i < N * nu; i++) {
-        S->zuL[i] = (!S->ufix[i] && hasb(S->ulo[i])) ? 1.0 : 0.0;
-        S->zuU[i] = (!S->ufix[i] && hasb(S->uhi[i])) ? 1.0 : 0.0;
+        S->zuL[i] = (!S->ufix[i] && hasb(S->ulo[i])) ? z0 : 0.0;
+        S->zuU[i] = (!S->ufix[i] && hasb(S->uhi[i])) ? z0 : 0.0;
     }
     for (int i = 0; i < N * ni; i++) {
-        S->vL[i] = hasb(S->clo[i]) ? 1.0 : 0.0;
-        S->vU[i] = hasb(S->chi[i]) ? 1.0 : 0.0;
+        S->vL[i] = hasb(S->clo[i]) ? z0 : 0.0;
+        S->vU[i] = hasb(S->chi[i]) ? z0 : 0.0;
+    }
+    if (warm && O->dual_in) {
+        const double *o = O->dual_in;
+        double *dst[] = {S->lam, S->yi, S->ye, S->zxL, S->zxU, S->zuL, S->zuU, S->vL, S->vU};
+        const size_t len[] = {(size_t)N * nx, NI, NE, NX1, NX1, NU, NU, NI, NI};
+        for (int a = 0; a < 9; a++) {
+            for (size_t i = 0; i < len[a]; i++)
+                dst[a][i] = a < 3 ? o[i] : (dst[a][i] > 0.0 ? fmax(o[i], 1e-3) : 0.0);
+            o += len[a];
+        }
     }
 
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;

@@ -108,6 +108,9 @@ typedef struct {
     const double *w0;      /* warm start (w layout) or NULL: q_k, qd_k (k >= 1) and F_k from w0, pushed
                               into their bounds; q_0, qd_0 stay the problem's (IPOPT warm_start_init_point
                               with x0 = the previous solution, RepeatedMPCwithThermal.py:445-448, 462-487) */
+    int warm_start;        /* with w0: IPOPT warm_start_init_point = yes -- warm_start_bound_push = _frac =
+                              1e-3 (slacks alike) and bound multipliers warm_start_mult_bound_push = 1e-3
+                              (CasADi's lam_x0 = 0 pushed), constraint multipliers 0 (lam_g0 = 0) */
 } mfo_opts;
 
 typedef struct {
@@ -135,6 +138,7 @@ typedef struct {
     /* kkt workspace */
     double *wv, *G;
     double mu;
+    double push_k;         /* bound_push = bound_frac of the initial point (cold 1e-2, warm 1e-3) */
 } ws_t;
 
 static int has(double b) { return isfinite(b); }
@@ -222,10 +226,11 @@ static void eval_derivs(ws_t *S, int k) {
 
 /* ------------------------------------------------------------------ */
 /* IPM                                                                 */
-#define PUSH_K1 1e-2
-#define PUSH_K2 1e-2
+/* IPOPT bound_push = bound_frac = 1e-2; warm_start_bound_push = _frac = 1e-3 (push_k) */
+#define PUSH_K1 push_k
+#define PUSH_K2 push_k
 
-static double push_into(double x, double lo, double hi) {
+static double push_into_k(double x, double lo, double hi, double push_k) {
     int hl = has(lo), hh = has(hi);
     if (hl && hh) {
         double pl = fmin(PUSH_K1 * fmax(1.0, fabs(lo)), PUSH_K2 * (hi - lo));
@@ -239,6 +244,7 @@ static double push_into(double x, double lo, double hi) {
     }
     return x;
 }
+#define push_into(x, lo, hi) push_into_k((x), (lo), (hi), S->push_k)
 
 static double *dalloc(size_t n) { return (double *)calloc(n ? n : 1, sizeof(double)); }
 
@@ -336,6 +342,9 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
     double h = P->h;
 
     /* ---- initial point ---- */
+    const int warm = O->warm_start && O->w0;
+    const double z0 = warm ? 1e-3 : 1.0;  /* bound_mult_init_val / warm_start_mult_bound_push */
+    S->push_k = 1e-2;
     for (int k = 0; k <= N; k++)
         for (int j = 0; j < n; j++) {
             double x = (k == 0 || !O->init_zero) ? P->q0[j] : 0.0;
@@ -347,6 +356,7 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
     for (int k = 0; k < N * nf; k++) S->Fv[k] = O->F_init;
     if (O->w0) {
         const int st = 2 * n + nf;
+        if (warm) S->push_k = 1e-3;
         for (int k = 0; k < N; k++) {
             const double *wk = O->w0 + n + (size_t)k * st;
             for (int j = 0; j < n; j++) {
@@ -362,15 +372,15 @@ int mfo_solve(const double *blob, const mfo_ocp *P, const mfo_opts *O, double *w
     }
     for (int k = 0; k <= N; k++)
         for (int j = 0; j < n; j++) {
-            S->zqL[k * n + j] = (k > 0 && has(QLO(j))) ? 1.0 : 0.0;
-            S->zqU[k * n + j] = (k > 0 && has(QHI(j))) ? 1.0 : 0.0;
+            S->zqL[k * n + j] = (k > 0 && has(QLO(j))) ? z0 : 0.0;
+            S->zqU[k * n + j] = (k > 0 && has(QHI(j))) ? z0 : 0.0;
         }
     for (int k = 0; k < N; k++)
         for (int j = 0; j < n; j++) {
-            S->zdL[k * n + j] = (k > 0 && has(DLO(j))) ? 1.0 : 0.0;
-            S->zdU[k * n + j] = (k > 0 && has(DHI(j))) ? 1.0 : 0.0;
-            S->vL[k * n + j] = has(TLO(k, j)) ? 1.0 : 0.0;
-            S->vU[k * n + j] = has(THI(k, j)) ? 1.0 : 0.0;
+            S->zdL[k * n + j] = (k > 0 && has(DLO(j))) ? z0 : 0.0;
+            S->zdU[k * n + j] = (k > 0 && has(DHI(j))) ? z0 : 0.0;
+            S->vL[k * n + j] = has(TLO(k, j)) ? z0 : 0.0;
+            S->vU[k * n + j] = has(THI(k, j)) ? z0 : 0.0;
         }
 
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;

@@ -101,7 +101,8 @@ class OCP(C.Structure):
 class Opts(C.Structure):
     _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
                 ("mu_init", C.c_double), ("init_zero", C.c_int), ("verbose", C.c_int),
-                ("prox", C.c_double), ("F_init", C.c_double), ("w0", C.POINTER(C.c_double))]
+                ("prox", C.c_double), ("F_init", C.c_double), ("w0", C.POINTER(C.c_double)),
+                ("warm_start", C.c_int)]
 
 
 class Result(C.Structure):
@@ -144,9 +145,11 @@ def make_ocp(spec: dict, model: Model):
 
 
 def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=200, mu_init=0.1, init_zero=False, verbose=False, prox=0.0,
-         F_init=0.0, w0=None):
-    """Solver options; w0 (w layout, optional) warm-starts q_k, qd_k (k >= 1) and F_k."""
-    o = Opts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), prox, F_init, None)
+         F_init=0.0, w0=None, warm_start=False):
+    """Solver options; w0 (w layout, optional) warm-starts q_k, qd_k (k >= 1) and F_k; warm_start: IPOPT's
+    warm_start_init_point constants for that start (mf_oracle.c mfo_opts.warm_start)."""
+    o = Opts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), prox, F_init, None,
+             int(warm_start))
     if w0 is not None:
         o._w0 = np.ascontiguousarray(w0, dtype=np.float64)  # kept alive with the struct
         o.w0 = o._w0.ctypes.data_as(C.POINTER(C.c_double))

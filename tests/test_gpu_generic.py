@@ -6,7 +6,10 @@ generic oracle (oracle/mf_ocp.c) and against the reference's own IPOPT trajector
 * C3 Box_Pilz_6DOF.py re-solved on the GPU from the reference's IK start matches plotter/solution.csv
   (G1, N=50), Result_2 (G2, N=80) and Result_1 (G4) to 1e-6 rad on every joint angle (SURVEY.md
   s.8c (vi)), and equals the oracle's solve
-* the thermal C2 variant (a8) = the oracle
+* Result_4 (G3, LeftConst) is a KKT point of the build's transcription: started there with IPOPT's
+  warm_start_init_point constants the GPU converges back to it (<= 1e-6 rad, equal objective)
+* the thermal C2 variant (a8) = the oracle; C4 at the committed fixture's horizon (N = 50, T = 2) and
+  with the 80 C winding bound active = the oracle
 """
 import numpy as np
 import pytest
@@ -100,6 +103,30 @@ def test_box_gpu_resolve_matches_reference(golden, name, kw):
     assert np.abs(ocp.q_traj(r.w[0]) - ocp.q_traj(w_or)).max() < 1e-7
 
 
+def test_box_gpu_g3_is_a_kkt_point(golden):
+    """G3 = plotter/Result_4/solution.csv (Box_Pilz_6DOF.py with LeftConst = True, N = 80).  The cold homotopy
+    reaches another local minimum (objective 1535.4 against G3's 1506.78): the problem has
+    several.  Started at G3 itself with IPOPT's warm_start_init_point constants and mu_0 = 1e-3, the GPU
+    solver converges back to G3: G3 is a KKT point of the build's transcription (E_0 <= 1e-8 within 1e-6
+    rad of it) with the same objective, and the device equals the oracle."""
+    g, N = golden["G3_box_N80"]
+    spec = PR.box_dual(q0=g[:12], N=N, left_const=True)
+    ocp = GOCP(spec)
+    kw = dict(w0=g, warm_start=True, mu_init=1e-3, max_iter=300, max_soc=4)
+    r = ocp.solve(**kw)
+    assert int(r.status[0]) == 0, (int(r.status[0]), int(r.iters[0]))
+    assert float(r.kkt[0]) <= 1e-8
+    dq = np.abs(ocp.q_traj(r.w[0]) - ocp.q_traj(g)).max()
+    assert dq < 1e-6, dq
+    one = PR.box_dual(N=1, q0=g[:12], left_const=True)
+    f_g3 = sum(G.node_derivs(one, g[k * 30:k * 30 + 30], np.zeros(18), np.zeros(1), np.zeros(12))[0][0]
+               for k in range(N))
+    assert abs(float(r.obj[0]) - f_g3) <= 1e-7 * abs(f_g3), (float(r.obj[0]), f_g3)
+    w_or, r_or = G.solve(spec, **kw)
+    assert r_or.status == 0 and abs(int(r.iters[0]) - r_or.iter) <= 2
+    np.testing.assert_allclose(r.w[0], w_or, atol=1e-7)
+
+
 def test_thermal_gpu_matches_oracle():
     spec = PR.pilz6_thermal(N=40, T0=79.0)
     ocp = GOCP(spec)
@@ -119,7 +146,7 @@ def _oracle_receding(spec, x0, steps, decimals, **kw):
     rnd = (lambda a: np.round(a, decimals)) if decimals is not None else (lambda a: a)
     for _ in range(steps):
         sp = dict(spec, q0=list(x[:n]), T0=list(x[n:]), qd0=list(u[:n]))
-        w, r = G.solve(sp, w0=prev, **kw)
+        w, r = G.solve(sp, w0=prev, warm_start=prev is not None, **kw)
         out.append((w, r))
         off = nx + (N - 1) * (nu + nx)
         xN = w[off + nu:off + nu + nx].copy()
@@ -222,8 +249,8 @@ def test_centauro_receding_horizon_gpu_matches_oracle():
     x, u, prev = x0, np.zeros(nu), None
     for s in range(steps):
         sp = PR.centauro(N=N, q0=x[:14], T0=x[14:], qd0=u[:14], target_decimals=(3 if s else -1))
-        w, r = G.solve(sp, w0=prev, **kw)
-        assert int(res[s].status[0]) == r.status, (s, int(res[s].status[0]), r.status)
+        w, r = G.solve(sp, w0=prev, warm_start=prev is not None, **kw)
+        assert int(res[s].status[0]) == r.status == 0, (s, int(res[s].status[0]), r.status)
         if r.status == 0:
             np.testing.assert_allclose(res[s].w[0], w, atol=1e-6, err_msg=f"step {s}")
         off = nx + (N - 1) * (nu + nx)
@@ -251,3 +278,42 @@ def test_box_shared_fatigue_gpu_matches_oracle(golden):
     np.testing.assert_allclose(ocp.q_traj(r.w[0]), ocp.q_traj(w_or), atol=1e-6)
     X = ocp.q_traj(r.w[0])
     assert (X[:, 12:].sum(1) <= spec["T_budget"] + 1e-6).all() and (X[:, 12:] <= spec["T_hi"] + 1e-6).all()
+
+
+def test_centauro_gpu_n50_fixture_horizon():
+    """C4 at BASELINE's N = 50 over the horizon of the committed Centauro fixture (Centauro_dynamics.py:90-91:
+    T = 2 s, N = 50; Const1 relative pose), thermal state included: GPU = oracle and the solution passes the
+    fixture's invariants (Euler continuity, force and moment balance, relative pose held)."""
+    from tests.test_centauro_cpu import check_solution
+
+    spec = PR.centauro(N=50, T=2.0)
+    ocp = GOCP(spec)
+    kw = dict(u_init=PR.centauro_u_init(spec), max_iter=500, max_soc=4)
+    r = ocp.solve(**kw)
+    w_ref, r_ref = G.solve(spec, **kw)
+    assert int(r.status[0]) == 0 and r_ref.status == 0, (int(r.status[0]), int(r.iters[0]), r_ref.status)
+    assert abs(int(r.iters[0]) - r_ref.iter) <= 2
+    np.testing.assert_allclose(r.w[0], w_ref, atol=1e-6)
+    check_solution(spec, r.w[0])
+
+
+def test_centauro_gpu_winding_bound_active():
+    """The 80 C winding bound (T in [0, 80], RepeatedMPCwithThermal.py:122-123, MPC_parameters.py:49) active:
+    C4 (N = 20, T = 30 s) with the windings starting at 79 C.  The bound holds at >= 10 (node, joint) pairs
+    and costs objective against the cold-winding solve (the solver re-poses the arms to shed load); GPU =
+    oracle, same active set."""
+    N = 20
+    cold = PR.centauro(N=N)
+    spec = PR.centauro(N=N, T0=79.0)
+    ocp = GOCP(spec)
+    kw = dict(u_init=PR.centauro_u_init(spec), max_iter=500, max_soc=4)
+    r = ocp.solve(**kw)
+    w_ref, r_ref = G.solve(spec, **kw)
+    assert int(r.status[0]) == 0 and r_ref.status == 0, (int(r.status[0]), int(r.iters[0]), r_ref.status)
+    np.testing.assert_allclose(r.w[0], w_ref, atol=1e-6)
+    T_gpu, T_or = ocp.q_traj(r.w[0])[:, 14:], ocp.q_traj(w_ref)[:, 14:]
+    act_gpu, act_or = T_gpu > 80.0 - 1e-5, T_or > 80.0 - 1e-5
+    assert act_gpu.sum() >= 10 and (act_gpu == act_or).all()
+    assert T_gpu.max() <= 80.0 + 1e-8
+    _, r_cold = G.solve(cold, **kw)
+    assert float(r.obj[0]) > r_cold.obj + 0.1
