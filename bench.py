@@ -46,15 +46,32 @@ FP64_PEAK_TFS = 78.6          # MI355X FP64 vector peak (spec)
 NODE_BYTES = 952
 
 
+def cpu_threads() -> tuple[int, str]:
+    """Threads for the all-cores CPU leg: the CPUs this process may run on (sched_getaffinity), capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box allots 16 host CPUs per GPU and exports
+    OMP_NUM_THREADS=16; os.cpu_count() there reports the whole host)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and 0 < int(env) < aff:
+        return int(env), f"OMP_NUM_THREADS={env} (the host share of this GPU); affinity allows {aff}, nproc {os.cpu_count()}"
+    return aff, f"every CPU of the process affinity ({aff}; nproc {os.cpu_count()})"
+
+
 def cpu_baseline(spec_of, Q0, lrefs, opts, threads: int, sample_mt: int, sample_1t: int, reps: int):
     """The CPU baseline (rank 0, N = 1): the same interior-point algorithm on the host -- the generic
     oracle IPM (oracle/mf_ocp.c) with the product's forward-over-reverse node functions compiled for
     the host (oracle/cpu_fast.cpp, -O3 AVX2/FMA) -- OpenMP over horizons on `threads` cores and on one
-    core; median of `reps` timed runs after one warm-up run.  Returns (record, CPU solutions)."""
+    core; median of `reps` timed runs after one warm-up run.  Also the phase split of the host solve
+    (node derivatives / KKT factorisation / directions / line search, mfg_time_get).
+    Returns (record, CPU solutions)."""
+    import ctypes as C
+
     from oracle import cpu_fast as CF
 
     specs = [spec_of(Q0[i], lrefs[i]) for i in range(max(sample_mt, sample_1t))]
     kw = dict(opts, **CF.FastNodes(specs[0]).opts_kw())
+    L = C.CDLL(CF.LIB)
+    L.mfg_time_get.argtypes = [C.POINTER(C.c_double)]
 
     def run(sp, nt):
         t0 = time.perf_counter()
@@ -65,19 +82,29 @@ def cpu_baseline(spec_of, Q0, lrefs, opts, threads: int, sample_mt: int, sample_
     for label, S, nt in (("all_cores", sample_mt, threads), ("one_core", sample_1t, 1)):
         run(specs[:min(S, nt)], nt)  # warm-up
         ts = []
+        L.mfg_time_reset()
         for _ in range(reps):
             dt, w, R = run(specs[:S], nt)
             ts.append(dt)
         conv = sum(1 for r in R if r.status == 0)
         out[label] = {"value": conv / float(np.median(ts)), "threads": nt, "horizons": S, "converged": conv,
                       "median_s": float(np.median(ts)), "runs_s": [round(t, 3) for t in ts]}
+        if label == "one_core":
+            a = (C.c_double * 5)()
+            L.mfg_time_get(a)
+            tot = max(a[4], 1e-12)
+            split = {"node_derivatives": a[0] / tot, "kkt_factorisation": a[1] / tot, "kkt_directions": a[2] / tot,
+                     "line_search": a[3] / tot, "other": (a[4] - a[0] - a[1] - a[2] - a[3]) / tot}
         if label == "all_cores":
             w_mt, st_mt = w, np.array([r.status for r in R])
     rec = {"value": out["all_cores"]["value"], "unit": "horizons/s", "cores": threads, "kind": "port",
            "single_core": out["one_core"]["value"], "nproc": os.cpu_count(), "detail": out,
+           "time_split_one_core": split,
            "sample": (f"first {sample_mt} horizons of the same batch on {threads} threads and the first {sample_1t} "
                       f"on 1 thread (median of {reps} runs after a warm-up); generic IPM oracle/mf_ocp.c with the "
-                      "product's node functions, both built for the host at -O3 -march=x86-64-v3 (oracle/libmfcpu.so)")}
+                      "product's node functions, both built for the host at -O3 -march=x86-64-v3 (oracle/libmfcpu.so); "
+                      "KKT by the block-tridiagonal Bunch-Kaufman factorisation (time_split_one_core gives its share; "
+                      "the GPU factors the same KKT by a Riccati recursion)")}
     return rec, w_mt, st_mt
 
 
@@ -143,18 +170,21 @@ def main() -> int:
     # stream), so the iteration tail of one step -- few horizons left, latency-bound kernels --
     # overlaps the bulk of the next.  Every step still solves the whole batch.
     inflight = max(1, args.inflight)
-    slots = [(ocp, stream, out, ptrs)]
+    # every slot solves on a stream of its own (none on the default stream, where the N > 1 gathers run)
+    slots = [(ocp, torch.cuda.Stream(dev), out, ptrs)]
     for _ in range(inflight - 1):
         ob = {k: torch.empty_like(v) for k, v in out.items()}
         slots.append((OCP(spec), torch.cuda.Stream(dev), ob, {k: v.data_ptr() for k, v in ob.items()}))
+    gathered = [None] * inflight  # event after the RCCL gather of each slot's last solutions
     torch.cuda.synchronize(dev)
 
     def solve_on(i):
         torch.cuda.set_device(dev)  # the HIP device is per host thread
         o, st, ob, pt = slots[i]
-        # N > 1: the RCCL gather of this slot's previous solutions was joined to the default stream;
-        # the new solve must not overwrite them before it has read them
-        st.wait_stream(torch.cuda.default_stream(dev))
+        # N > 1: the new solve must not overwrite this slot's previous solutions before their gather has
+        # read them; it waits for that gather alone, not for other slots' work
+        if gathered[i] is not None:
+            st.wait_event(gathered[i])
         o.solve_dev(q0.data_ptr(), lref.data_ptr(), hi - lo, pt, stream=st.cuda_stream, **opts)
         st.synchronize()
 
@@ -166,8 +196,12 @@ def main() -> int:
                 if s_ >= inflight:  # step s_ - inflight done: its slot is free (gather its solutions)
                     futs[s_ - inflight].result()
                     if world > 1:
-                        _, _, ob, _ = slots[(s_ - inflight) % inflight]
+                        i = (s_ - inflight) % inflight
+                        _, _, ob, _ = slots[i]
                         gather_solutions(ob["w"], ob["status"], rank, world)
+                        ev = torch.cuda.Event()
+                        ev.record(torch.cuda.current_stream(dev))  # the stream the gather ran on
+                        gathered[i] = ev
                 if s_ < K:
                     futs.append(ex.submit(solve_on, s_ % inflight))
 
@@ -275,12 +309,13 @@ def main() -> int:
         def timed(nb, reps):
             o = {k: v[:nb] for k, v in out.items()}
             pt = {k: v.data_ptr() for k, v in o.items()}
-            ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=stream.cuda_stream, **opts)
+            s0 = slots[0][1]
+            ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=s0.cuda_stream, **opts)
             ts = []
             for _ in range(reps):
                 torch.cuda.synchronize(dev)
                 t = time.perf_counter()
-                ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=stream.cuda_stream, **opts)
+                ocp.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=s0.cuda_stream, **opts)
                 torch.cuda.synchronize(dev)
                 ts.append(time.perf_counter() - t)
             return float(np.median(ts)), int((o["status"] == 0).sum().item())
@@ -296,7 +331,7 @@ def main() -> int:
         from oracle import pin_np as P
         from oracle.urdf_np import load_urdf_file
 
-        threads = min(16, os.cpu_count() or 1)
+        threads, why = cpu_threads()
         S = args.cpu_sample or 4 * threads
         ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
         Qs = Q0_all[:S]
@@ -309,6 +344,7 @@ def main() -> int:
         both = (st_gpu == 0) & (st_cpu == 0)
         wq = lambda w: np.concatenate([w[:, :n]] + [w[:, n + k * (2 * n + ocp.nf) + n + ocp.nf:
                                                        n + (k + 1) * (2 * n + ocp.nf)] for k in range(N)], axis=1)
+        rec["cores_note"] = why
         rec["gpu_vs_cpu"] = {"horizons": S, "both_converged": int(both.sum()),
                              "same_status": int((st_gpu == st_cpu).sum()),
                              "max_dq": float(np.abs(wq(w_gpu[both]) - wq(w_cpu[both])).max()) if both.any() else None}

@@ -372,6 +372,15 @@ struct DBuf {
     double *p = nullptr;
     ~DBuf() { if (p) (void)hipFree(p); }
 };
+struct IBuf {
+    int *p = nullptr;
+    ~IBuf() { if (p) (void)hipFree(p); }
+};
+// a host-path call's own stream (destroyed on every return path)
+struct OwnStream {
+    hipStream_t s = nullptr;
+    ~OwnStream() { if (s) { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); } }
+};
 static int dalloc(DBuf &b, size_t n) {
     HIPCHK(hipMalloc(&b.p, (n ? n : 1) * sizeof(double)));
     return MF_OK;
@@ -675,29 +684,28 @@ static int solve_host(mf_problem *p, int batch, const double *q0, const double *
     HIPCHK(hipSetDevice(device));
     const int n = p->C.n, ws = mf_problem_wsize(p);
     DBuf dq0, dqd0, dw0, dl, dw, dk, dob;
-    int *dst = nullptr, *dit = nullptr;
+    IBuf dst, dit;
     if ((e = h2d(dq0, q0, (size_t)n * batch))) return e;
     if (qd0 && (e = h2d(dqd0, qd0, (size_t)n * batch))) return e;
     if (w0 && (e = h2d(dw0, w0, (size_t)ws * batch))) return e;
     if (line_ref && (e = h2d(dl, line_ref, 2 * (size_t)batch))) return e;
     if ((e = dalloc(dw, (size_t)ws * batch)) || (e = dalloc(dk, batch)) || (e = dalloc(dob, batch))) return e;
-    HIPCHK(hipMalloc(&dst, sizeof(int) * batch));
-    HIPCHK(hipMalloc(&dit, sizeof(int) * batch));
-    e = solve_core(p, batch, dq0.p, dqd0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst, dit, dk.p, dob.p, nullptr);
-    if (!e) {
-        hipError_t he = hipDeviceSynchronize();
-        if (he != hipSuccess) e = fail(MF_ERR_DEVICE, hipGetErrorString(he));
-    }
-    if (!e) {
-        (void)hipMemcpy(w, dw.p, sizeof(double) * ws * (size_t)batch, hipMemcpyDeviceToHost);
-        if (status) (void)hipMemcpy(status, dst, sizeof(int) * batch, hipMemcpyDeviceToHost);
-        if (iters) (void)hipMemcpy(iters, dit, sizeof(int) * batch, hipMemcpyDeviceToHost);
-        if (kkt) (void)hipMemcpy(kkt, dk.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
-        if (obj) (void)hipMemcpy(obj, dob.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
-    }
-    (void)hipFree(dst);
-    (void)hipFree(dit);
-    return e;
+    HIPCHK(hipMalloc(&dst.p, sizeof(int) * batch));
+    HIPCHK(hipMalloc(&dit.p, sizeof(int) * batch));
+    // a stream of this call's own: the solve and the copies back synchronise with it alone, so host
+    // calls on other handles / streams of the device keep running (one handle per stream, reentrant)
+    OwnStream os;
+    HIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
+    e = solve_core(p, batch, dq0.p, dqd0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst.p, dit.p, dk.p, dob.p,
+                   os.s);
+    if (e) return e;
+    HIPCHK(hipMemcpyAsync(w, dw.p, sizeof(double) * ws * (size_t)batch, hipMemcpyDeviceToHost, os.s));
+    if (status) HIPCHK(hipMemcpyAsync(status, dst.p, sizeof(int) * batch, hipMemcpyDeviceToHost, os.s));
+    if (iters) HIPCHK(hipMemcpyAsync(iters, dit.p, sizeof(int) * batch, hipMemcpyDeviceToHost, os.s));
+    if (kkt) HIPCHK(hipMemcpyAsync(kkt, dk.p, sizeof(double) * batch, hipMemcpyDeviceToHost, os.s));
+    if (obj) HIPCHK(hipMemcpyAsync(obj, dob.p, sizeof(double) * batch, hipMemcpyDeviceToHost, os.s));
+    HIPCHK(hipStreamSynchronize(os.s));
+    return MF_OK;
 }
 extern "C" int mf_solve_batch(mf_problem *p, int batch, const double *q0, const double *line_ref,
                               const mf_solver_opts *opts, double *w, int *status, int *iters, double *kkt, double *obj,

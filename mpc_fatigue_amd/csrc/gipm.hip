@@ -1076,6 +1076,7 @@ struct mf_gproblem {
     DevFrame *dF0 = nullptr, *dF1 = nullptr;
     double *d_ulo = nullptr, *d_uhi = nullptr, *d_clo = nullptr, *d_chi = nullptr;
     int cap = 0;
+    int last_batch = 0;  // batch of the last solve (diagnostic reads are bounded by it)
     std::vector<double *> bufs;
     GArrays A;
     GState *d_st = nullptr;
@@ -1153,6 +1154,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     P.F_init = o ? o->F_init : 0.0;
     P.max_soc = o ? o->max_soc : 4;
     P.warm_start = (o && d_w0) ? o->warm_start : 0;
+    p->last_batch = batch;
     P.has_u_init = (o && o->u_init) ? 1 : 0;
     if (P.has_u_init)
         for (int j = 0; j < D::NU; j++) P.u_init[j] = o->u_init[j];
@@ -1346,6 +1348,14 @@ struct GBuf {
     double *p = nullptr;
     ~GBuf() { if (p) (void)hipFree(p); }
 };
+struct GIBuf {
+    int *p = nullptr;
+    ~GIBuf() { if (p) (void)hipFree(p); }
+};
+struct GOwnStream {
+    hipStream_t s = nullptr;
+    ~GOwnStream() { if (s) { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); } }
+};
 int gh2d(GBuf &b, const double *h, size_t n) {
     GHIPCHK(hipMalloc(&b.p, n * sizeof(double)));
     GHIPCHK(hipMemcpy(b.p, h, n * sizeof(double), hipMemcpyHostToDevice));
@@ -1366,30 +1376,27 @@ extern "C" int mf_gsolve_batch(mf_gproblem *p, int batch, const double *x0, cons
     GHIPCHK(hipSetDevice(device));
     const int ws = p->nx + p->spec.N * (p->nu + p->nx);
     GBuf dx0, du0, dw0, dl, dw, dk, dob;
-    int *dst = nullptr, *dit = nullptr;
+    GIBuf dst, dit;
     if ((e = gh2d(dx0, x0, (size_t)p->nx * batch))) return e;
     if (u0 && (e = gh2d(du0, u0, (size_t)p->nu * batch))) return e;
     if (w0 && (e = gh2d(dw0, w0, (size_t)ws * batch))) return e;
     if (line_ref && (e = gh2d(dl, line_ref, 2 * (size_t)batch))) return e;
     if ((e = galloc(dw, (size_t)ws * batch)) || (e = galloc(dk, batch)) || (e = galloc(dob, batch))) return e;
-    GHIPCHK(hipMalloc(&dst, sizeof(int) * batch));
-    GHIPCHK(hipMalloc(&dit, sizeof(int) * batch));
-    e = gdispatch_solve(p, batch, dx0.p, du0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst, dit, dk.p, dob.p,
-                        nullptr);
-    if (!e) {
-        hipError_t he = hipDeviceSynchronize();
-        if (he != hipSuccess) e = capi_fail(MF_ERR_DEVICE, hipGetErrorString(he));
-    }
-    if (!e) {
-        (void)hipMemcpy(w, dw.p, sizeof(double) * ws * (size_t)batch, hipMemcpyDeviceToHost);
-        if (status) (void)hipMemcpy(status, dst, sizeof(int) * batch, hipMemcpyDeviceToHost);
-        if (iters) (void)hipMemcpy(iters, dit, sizeof(int) * batch, hipMemcpyDeviceToHost);
-        if (kkt) (void)hipMemcpy(kkt, dk.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
-        if (obj) (void)hipMemcpy(obj, dob.p, sizeof(double) * batch, hipMemcpyDeviceToHost);
-    }
-    (void)hipFree(dst);
-    (void)hipFree(dit);
-    return e;
+    GHIPCHK(hipMalloc(&dst.p, sizeof(int) * batch));
+    GHIPCHK(hipMalloc(&dit.p, sizeof(int) * batch));
+    // this call's own stream: synchronising it leaves other handles / streams of the device running
+    GOwnStream os;
+    GHIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
+    e = gdispatch_solve(p, batch, dx0.p, du0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst.p, dit.p, dk.p,
+                        dob.p, os.s);
+    if (e) return e;
+    GHIPCHK(hipMemcpyAsync(w, dw.p, sizeof(double) * ws * (size_t)batch, hipMemcpyDeviceToHost, os.s));
+    if (status) GHIPCHK(hipMemcpyAsync(status, dst.p, sizeof(int) * batch, hipMemcpyDeviceToHost, os.s));
+    if (iters) GHIPCHK(hipMemcpyAsync(iters, dit.p, sizeof(int) * batch, hipMemcpyDeviceToHost, os.s));
+    if (kkt) GHIPCHK(hipMemcpyAsync(kkt, dk.p, sizeof(double) * batch, hipMemcpyDeviceToHost, os.s));
+    if (obj) GHIPCHK(hipMemcpyAsync(obj, dob.p, sizeof(double) * batch, hipMemcpyDeviceToHost, os.s));
+    GHIPCHK(hipStreamSynchronize(os.s));
+    return MF_OK;
 }
 
 template <class FAM>
@@ -1420,7 +1427,7 @@ template <class FAM> static int gdual_core(mf_gproblem *p, int b, double *out) {
     using D = typename FAM::D;
     const GSz<D> Z(p->spec.N);
     const GArrays &A = p->A;
-    if (b < 0 || b >= p->cap) return capi_fail(MF_ERR_ARG, "problem index out of range");
+    if (b < 0 || b >= p->last_batch) return capi_fail(MF_ERR_ARG, "problem index out of range (last solve's batch)");
     double *src[] = {A.lam, A.yi, A.ye, A.zxL, A.zxU, A.zuL, A.zuU, A.vL, A.vU};
     const size_t len[] = {Z.l(), Z.i(), Z.e(), Z.x(), Z.x(), Z.u(), Z.u(), Z.i(), Z.i()};
     size_t off = 0;

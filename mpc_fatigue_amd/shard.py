@@ -18,20 +18,32 @@ def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def gather_solutions(w, status, rank: int, world: int, dst: int = 0):
+def gather_solutions(w, status, rank: int, world: int, dst: int = 0, total: int | None = None):
     """Gather every rank's solution block to `dst`; returns (W, S) on dst, (None, None) elsewhere.
 
-    Shards must have equal size (the bench uses batch-per-GPU shards).
+    Shards may differ in size by one horizon (shard_range of a total not divisible by world): every
+    rank pads its block to the largest shard (ceil(total / world) rows), the gather moves equal
+    blocks, and dst drops each rank's padding.  total defaults to world x this rank's rows (equal
+    shards, the bench's batch-per-GPU shards).
     """
     import torch
     import torch.distributed as dist
 
     if world == 1:
         return w, status
+    rows = w.shape[0]
+    total = rows * world if total is None else total
+    sizes = [shard_range(total, world, r)[1] - shard_range(total, world, r)[0] for r in range(world)]
+    if sizes[rank] != rows:
+        raise ValueError(f"rank {rank} holds {rows} rows, shard_range({total}, {world}) gives {sizes[rank]}")
+    m = max(sizes)
+    if rows < m:
+        w = torch.cat([w, w.new_zeros((m - rows,) + tuple(w.shape[1:]))])
+        status = torch.cat([status, status.new_full((m - rows,), -1)])
     ws = [torch.empty_like(w) for _ in range(world)] if rank == dst else None
     ss = [torch.empty_like(status) for _ in range(world)] if rank == dst else None
-    dist.gather(w, ws, dst=dst)
-    dist.gather(status, ss, dst=dst)
+    dist.gather(w.contiguous(), ws, dst=dst)
+    dist.gather(status.contiguous(), ss, dst=dst)
     if rank == dst:
-        return torch.cat(ws), torch.cat(ss)
+        return torch.cat([x[:n] for x, n in zip(ws, sizes)]), torch.cat([x[:n] for x, n in zip(ss, sizes)])
     return None, None

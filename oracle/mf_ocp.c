@@ -35,6 +35,19 @@
 
 #include "hd_kin.h"
 
+/* Where the host IPM's time goes (bench.py cpu_baseline split): seconds summed over every solve since
+ * the last mfg_time_reset, per phase: 0 node derivatives, 1 KKT factorisation (every inertia try),
+ * 2 Newton directions (incl. second-order corrections), 3 line-search merit evaluations, 4 total. */
+#include <time.h>
+static double g_tsplit[5];
+static double wall_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + 1e-9 * t.tv_nsec;
+}
+void mfg_time_reset(void) { memset(g_tsplit, 0, sizeof g_tsplit); }
+void mfg_time_get(double *out5) { memcpy(out5, g_tsplit, sizeof g_tsplit); }
+
 #define GX 32              /* max state size */
 #define GU 32              /* max control size */
 #define GV (GX + GU)       /* max node variables */
@@ -952,12 +965,15 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     double E0 = INFINITY, cviol = INFINITY;
     const int has_tier1 = P->tier1_to > P->tier1_from;
 
+    double ts[5] = {0, 0, 0, 0, 0}, t_solve0 = wall_s(), t_ph;
     for (it = 0; it <= O->max_iter; it++) {
         /* ---- node derivatives ---- */
+        t_ph = wall_s();
 #ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 1)
 #endif
         for (int k = 0; k < N; k++) eval_derivs(S, k);
+        ts[0] += wall_s() - t_ph;
 
         /* ---- optimality error (IPOPT E_0 with s_max scaling) ---- */
         double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sum_mult = 0, sum_bmult = 0;
@@ -1085,7 +1101,9 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
         if (reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
         if (tier == 1) d1 = reg; else if (tier == 2) dw = reg;
         for (tries = 0; tries < 60; tries++) {
+            t_ph = wall_s();
             const int fr = kkt_factor(S, dw, dc, d1);
+            ts[1] += wall_s() - t_ph;
             if (fr == 0) { factor_ok = 1; break; }
             if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
             n_ic++;
@@ -1110,7 +1128,9 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
 
         /* ---- Newton direction for the residuals of the current point ---- */
         residuals_cached(S, S->rdyn, S->rin, S->req);
+        t_ph = wall_s();
         kkt_direction(S, mu, S->rdyn, S->rin, S->req);
+        ts[2] += wall_s() - t_ph;
         double ap, az;
         ftb(S, tau_fb, &ap, &az);
         if (O->verbose > 2) ftb_report(S, tau_fb);
@@ -1133,7 +1153,9 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
             double ph, th;
             int okk;
             trial_point(S, alpha);
+            t_ph = wall_s();
             merit_parts(S, S->tx, S->tu, S->ts, mu, &ph, &th, &okk, S->trdyn, S->trin, S->treq);
+            ts[3] += wall_s() - t_ph;
             const double mt = ph + nu_pen * th;
             if (okk && isfinite(mt) && mt - m0 <= eta * alpha * fmin(Dphi, 0.0) + slack_m) { accepted = 1; break; }
             /* IPOPT A-5.5..A-5.9: second-order corrections after the first trial step when it raised the
@@ -1145,13 +1167,17 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
                 for (size_t i = 0; i < (size_t)N * ne; i++) S->seq[i] = alpha * S->req[i] + S->treq[i];
                 for (int p = 0; p < O->max_soc; p++) {
                     save_direction(S);
+                    t_ph = wall_s();
                     kkt_direction(S, mu, S->sdyn, S->sin_, S->seq);
+                    ts[2] += wall_s() - t_ph;
                     double aps, azs;
                     ftb(S, tau_fb, &aps, &azs);
                     trial_point(S, aps);
                     double phs, ths;
                     int oks;
+                    t_ph = wall_s();
                     merit_parts(S, S->tx, S->tu, S->ts, mu, &phs, &ths, &oks, S->trdyn, S->trin, S->treq);
+                    ts[3] += wall_s() - t_ph;
                     const double ms = phs + nu_pen * ths;
                     if (O->verbose > 1)
                         fprintf(stderr, "      soc %d a %.3e th %.3e (th0 %.3e) m %.10e (m0 %.10e)\n", p, aps, ths, th0, ms, m0);
@@ -1203,6 +1229,13 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
             if (hasb(S->chi[i])) ZUPD(S->vU[i], S->dvU[i], S->chi[i] - S->s[i]);
         }
 #undef ZUPD
+    }
+    ts[4] = wall_s() - t_solve0;
+    for (int i = 0; i < 5; i++) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+        g_tsplit[i] += ts[i];
     }
     /* ---- output in the reference layout [x_0 | (u_k, x_{k+1}) x N] ---- */
     if (w_out) {

@@ -29,24 +29,25 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, total):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    lo, hi = shard_range(8 * world, world, rank)
+    lo, hi = shard_range(total, world, rank)
     w = torch.arange(lo * 5, hi * 5, dtype=torch.float64).reshape(hi - lo, 5)
     st = torch.full((hi - lo,), rank, dtype=torch.int32)
-    W, S = gather_solutions(w, st, rank, world)
+    W, S = gather_solutions(w, st, rank, world, total=total)
     if rank == 0:
         q.put((W.numpy().tolist(), S.numpy().tolist()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gather_solutions_gloo(world):
+@pytest.mark.parametrize("world,total", [(2, 16), (2, 17)])
+def test_gather_solutions_gloo(world, total):
+    """Equal shards and unequal ones (17 horizons over 2 ranks: 9 + 8, padded for the gather)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, total)) for r in range(world)]
     for p in procs:
         p.start()
     W, S = q.get(timeout=120)
@@ -55,9 +56,10 @@ def test_gather_solutions_gloo(world):
         assert p.exitcode == 0
     import numpy as np
     W = np.array(W)
-    assert W.shape == (8 * world, 5)
-    np.testing.assert_array_equal(W.reshape(-1), np.arange(8 * world * 5))
-    assert S == [r for r in range(world) for _ in range(8)]
+    assert W.shape == (total, 5)
+    np.testing.assert_array_equal(W.reshape(-1), np.arange(total * 5))
+    spans = [shard_range(total, world, r) for r in range(world)]
+    assert S == [r for r in range(world) for _ in range(spans[r][1] - spans[r][0])]
 
 
 def _solve_worker(rank, world, port, q):
