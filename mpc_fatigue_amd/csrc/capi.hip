@@ -517,6 +517,7 @@ extern "C" int mf_problem_create(const mf_model *mc, const mf_problem_spec *spec
     memcpy(C.qd_hi, spec->qd_hi, sizeof C.qd_hi);
     memcpy(C.q_lo, spec->q_lo, sizeof C.q_lo);
     memcpy(C.q_hi, spec->q_hi, sizeof C.q_hi);
+    C.kkt_lanes = 32;
     *out = p;
     return MF_OK;
 }
@@ -535,7 +536,10 @@ extern "C" int mf_problem_wsize(const mf_problem *p) {
     return p->C.n + p->C.N * (2 * p->C.n + p->C.nf);
 }
 
-static int ensure_ws(mf_problem *p, int batch) {
+// s: the solve's stream.  The workspace is zeroed on it, so the solve's kernels are ordered after the
+// zeroing (a hipMemset on the legacy null stream is asynchronous and does not order a non-blocking stream:
+// a first solve on a torch stream then raced it).
+static int ensure_ws(mf_problem *p, int batch, hipStream_t s) {
     int e = upload_model(p->model);
     if (e) return e;
     if (!p->d_frame && (e = frame_dev(p->model, p->spec.frame, &p->d_frame))) return e;
@@ -568,9 +572,9 @@ static int ensure_ws(mf_problem *p, int batch) {
             free_ws(p);
             return fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
         }
-        (void)hipMemset(ptr, 0, it.n * (size_t)batch * sizeof(double));
         p->bufs.push_back(ptr);
         *it.ptr = ptr;
+        HIPCHK(hipMemsetAsync(ptr, 0, it.n * (size_t)batch * sizeof(double), s));
     }
     HIPCHK(hipMalloc(&p->d_st, sizeof(ProbState) * (size_t)batch));
     HIPCHK(hipMalloc(&p->d_active, sizeof(int)));
@@ -588,7 +592,7 @@ static int ensure_ws(mf_problem *p, int batch) {
 static int solve_core(mf_problem *p, int batch, const double *d_q0, const double *d_qd0, const double *d_w0,
                       const double *d_lref, const mf_solver_opts *o,
                       double *d_w, int *d_status, int *d_iters, double *d_kkt, double *d_obj, hipStream_t s) {
-    int e = ensure_ws(p, batch);
+    int e = ensure_ws(p, batch, s);
     if (e) return e;
     OcpConst C = p->C;
     C.tol = o ? o->tol : 1e-8;
@@ -823,6 +827,14 @@ extern "C" int mf_problem_timing(mf_problem *p, int enable) {
     p->timing = enable ? 1 : 0;
     for (int k = 0; k < MF_NKERNELS; k++) { p->t_ms[k] = 0; p->t_launch[k] = 0; }
     return MF_OK;
+}
+
+extern "C" int mf_problem_kkt_lanes(mf_problem *p, int lanes) {
+    if (!p) return fail(MF_ERR_ARG, "null problem");
+    if (lanes == 0) return p->C.kkt_lanes;
+    if (lanes != 32 && lanes != 64) return fail(MF_ERR_ARG, "kkt lanes must be 32 or 64");
+    p->C.kkt_lanes = lanes;
+    return lanes;
 }
 
 extern "C" const char *mf_kernel_name(int slot) {

@@ -1109,7 +1109,8 @@ static void gfree_ws(mf_gproblem *p) {
     p->cap = 0;
 }
 
-template <class FAM> static int gensure_ws(mf_gproblem *p, int batch) {
+// the workspace is zeroed on the solve's stream s (ordering as capi.hip ensure_ws)
+template <class FAM> static int gensure_ws(mf_gproblem *p, int batch, hipStream_t s) {
     if (p->cap >= batch) return MF_OK;
     gfree_ws(p);
     std::vector<std::pair<double **, size_t>> items;
@@ -1122,9 +1123,9 @@ template <class FAM> static int gensure_ws(mf_gproblem *p, int batch) {
             gfree_ws(p);
             return capi_fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
         }
-        (void)hipMemset(ptr, 0, it.second * (size_t)batch * sizeof(double));
         p->bufs.push_back(ptr);
         *it.first = ptr;
+        GHIPCHK(hipMemsetAsync(ptr, 0, it.second * (size_t)batch * sizeof(double), s));
     }
     GHIPCHK(hipMalloc(&p->d_st, sizeof(GState) * (size_t)batch));
     GHIPCHK(hipMalloc(&p->d_active, sizeof(int)));
@@ -1143,7 +1144,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
                        const double *d_lref, const mf_gopts *o, double *d_w, int *d_status, int *d_iters,
                        double *d_kkt, double *d_obj, hipStream_t s) {
     using D = typename FAM::D;
-    int e = gensure_ws<FAM>(p, batch);
+    int e = gensure_ws<FAM>(p, batch, s);
     if (e) return e;
     GParams P = p->P;
     P.tol = o ? o->tol : 1e-8;

@@ -1,0 +1,124 @@
+"""Throughput of the generic device solver (csrc/gipm.hip) on BASELINE configs 3 and 4, batched over
+perturbed initial states (bench.py imports generic_extra for its `generic` keys; run alone for a probe):
+
+    python tools/generic_bench.py [--batch 1024] [--sample 2]
+
+C3-shared: problems.box_shared_fatigue(N=100) from the reference's IK start q0 (tests/golden G1) with
+  q0_i = q0 + U(-0.01, 0.01) per joint; the equilibrium-tolerance homotopy (pos_toll 1 -> 1e-2 -> 1e-4,
+  each stage warm-started from the previous one), i.e. what GOCP.solve_box does, timed end to end.
+C4: problems.centauro(N=50, T=2) (the committed Centauro fixture's horizon, Centauro_dynamics.py:90-91)
+  from the IK start with q0_i = q0 + U(-0.02, 0.02), one solve from the reference's sol0 controls.
+A horizon counts when its last stage converged (E_0 <= 1e-8).  GPU-vs-CPU: the first `sample` horizons
+solved by the host IPM (oracle/libmfcpu.so, the same algorithm) and compared on the state trajectories.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def _golden_q0():
+    g = np.loadtxt(os.path.join(ROOT, "tests", "golden", "G1_box_N50_solution.csv"), delimiter=",")
+    return g[:12]
+
+
+def _x_traj(w, nx, nu, N):
+    w = np.atleast_2d(w)
+    return np.concatenate([w[:, None, :nx], w[:, nx:].reshape(w.shape[0], N, nu + nx)[:, :, nu:]], axis=1)
+
+
+def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0) -> dict:
+    import torch
+
+    from mpc_fatigue_amd import problems as PR
+    from mpc_fatigue_amd.gocp import GOCP
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    stream = torch.cuda.current_stream(dev)
+    rng = np.random.default_rng(seed)
+    out = {}
+    cases = []
+    q0b = _golden_q0()
+    sp3 = PR.box_shared_fatigue(N=100, q0=q0b)
+    X3 = np.hstack([q0b[None] + rng.uniform(-0.01, 0.01, (batch, 12)), np.tile(sp3["T0"], (batch, 1))])
+    cases.append(("c3_shared_budget_n100", sp3, X3, [dict(sp3, pos_toll=t) for t in PR.box_homotopy_tolerances()],
+                  dict(u_init=PR.box_u_init(sp3), max_iter=1000, max_soc=4)))
+    sp4 = PR.centauro(N=50, T=2.0)
+    q0c = np.asarray(sp4["q0"])
+    X4 = np.hstack([q0c[None] + rng.uniform(-0.02, 0.02, (batch, 14)), np.tile(sp4["T0"], (batch, 1))])
+    cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(u_init=PR.centauro_u_init(sp4), max_iter=500, max_soc=4)))
+    for name, spec, X, stages, kw in cases:
+        gs = [GOCP(st) for st in stages]
+        nx, nu, N = gs[0].nx, gs[0].nu, spec["N"]
+        x = torch.as_tensor(X, dtype=torch.float64, device=dev).contiguous()
+        bufs = [{"w": torch.empty((batch, gs[0].wsize), dtype=torch.float64, device=dev),
+                 "status": torch.empty(batch, dtype=torch.int32, device=dev),
+                 "iters": torch.empty(batch, dtype=torch.int32, device=dev),
+                 "kkt": torch.empty(batch, dtype=torch.float64, device=dev),
+                 "obj": torch.empty(batch, dtype=torch.float64, device=dev)} for _ in stages]
+
+        def run():
+            prev = None
+            iters = []
+            for g, ob in zip(gs, bufs):
+                ptr = {k: v.data_ptr() for k, v in ob.items()}
+                g.solve_dev(x.data_ptr(), None, None if prev is None else prev.data_ptr(), None, batch, ptr,
+                            stream=stream.cuda_stream, **kw)
+                prev = ob["w"]
+            torch.cuda.synchronize(dev)
+
+        run()  # warm-up (workspaces)
+        t0 = time.perf_counter()
+        run()
+        dt = time.perf_counter() - t0
+        st = bufs[-1]["status"].cpu().numpy()
+        its = [int(b["iters"].sum().item()) for b in bufs]
+        conv = int((st == 0).sum())
+        rec = {"value": conv / dt, "unit": "horizons/s", "batch": batch, "converged": conv,
+               "converged_frac": conv / batch, "seconds": dt, "stages": len(stages),
+               "mean_iters_per_stage": [i / batch for i in its], "N": N, "nx": nx, "nu": nu, "ni": gs[0].ni}
+        if cpu and sample > 0:
+            from oracle import cpu_fast as CF
+            from oracle import generic as G
+            fk = CF.FastNodes(spec)
+            w = None
+            t1 = time.perf_counter()
+            for st_spec in stages:
+                specs = [dict(st_spec, q0=list(X[i, :len(spec["q0"])]), T0=list(X[i, len(spec["q0"]):]))
+                         for i in range(sample)]
+                kwc = dict(kw, **fk.opts_kw())
+                if w is not None:
+                    res = [G.solve_batch([s], L=CF.lib(), w0=w[i], **kwc) for i, s in enumerate(specs)]
+                    w = np.vstack([r[0] for r in res])
+                    R = [r[1][0] for r in res]
+                else:
+                    w, R = CF.solve_batch(specs, nthreads=min(sample, 16), **kwc)
+            tc = time.perf_counter() - t1
+            wg = bufs[-1]["w"][:sample].cpu().numpy()
+            both = np.array([r.status == 0 for r in R]) & (st[:sample] == 0)
+            rec["gpu_vs_cpu"] = {"horizons": sample, "both_converged": int(both.sum()),
+                                 "max_dx": (float(np.abs(_x_traj(wg[both], nx, nu, N) - _x_traj(w[both], nx, nu, N)).max())
+                                            if both.any() else None),
+                                 "cpu_seconds": tc}
+        out[name] = rec
+        print(f"[generic_bench] {name}: {json.dumps(rec)}", file=sys.stderr, flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--sample", type=int, default=2)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.init()
+    print(json.dumps(generic_extra(a.batch, a.sample)))
