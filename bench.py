@@ -121,7 +121,6 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="horizons in the CPU sample (0: 4 per thread)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU runs (median reported)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1024-shard and single-problem figures")
-    ap.add_argument("--kkt-lanes", type=int, default=0, help="Riccati kernel lanes per horizon (32/64; 0: library default)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent steps in flight (own workspace, stream and host thread each)")
     args = ap.parse_args()
@@ -176,9 +175,6 @@ def main() -> int:
     for _ in range(inflight - 1):
         ob = {k: torch.empty_like(v) for k, v in out.items()}
         slots.append((OCP(spec), torch.cuda.Stream(dev), ob, {k: v.data_ptr() for k, v in ob.items()}))
-    if args.kkt_lanes:
-        for sl in slots:
-            sl[0].kkt_lanes(args.kkt_lanes)
     gathered = [None] * inflight  # event after the RCCL gather of each slot's last solutions
     torch.cuda.synchronize(dev)
 
@@ -301,7 +297,7 @@ def main() -> int:
                    "parallelism": f"dp{world} (independent horizons; RCCL gather of solutions)",
                    "converged_per_step": converged, "converged_frac": converged / gB,
                    "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
-                   "steps_in_flight": inflight, "kkt_lanes_per_horizon": ocp.kkt_lanes(),
+                   "steps_in_flight": inflight,
                    "tol": opts["tol"]},
         "roofline": roofline,
         "tail": tail_rec,

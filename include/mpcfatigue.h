@@ -169,10 +169,6 @@ int mf_problem_kernel_stats(const mf_problem *p, double *ms_total, long *launche
  * Fills up to `cap` entries of the non-null arrays; returns the number of chunks. */
 int mf_problem_trace(const mf_problem *p, int *iter, int *running, double *ms, int cap);
 const char *mf_kernel_name(int slot);
-/* Lanes per horizon of the Riccati kernel (k_ipm_kkt): 32 = two horizons per wavefront (default), 64 =
- * one horizon per wavefront.  Both run the same arithmetic in the same order (bit-identical iterates).
- * lanes = 0 queries.  Returns the setting or MF_ERR_ARG. */
-int mf_problem_kkt_lanes(mf_problem *p, int lanes);
 
 /* ---- generic stage-structured OCPs: dual-arm box (C3), thermal fatigue state (a8), Centauro (C4) ----
  * Replaces the per-node transcription loops of python/2_pilz_6_DOF/Box_Pilz_6DOF.py:219-456 and of

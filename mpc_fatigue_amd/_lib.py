@@ -118,7 +118,6 @@ def lib() -> C.CDLL:
         "mf_problem_kernel_stats": ([vp, dp, C.POINTER(C.c_long)], C.c_int),
         "mf_problem_trace": ([vp, ip, ip, dp, C.c_int], C.c_int),
         "mf_kernel_name": ([C.c_int], cp),
-        "mf_problem_kkt_lanes": ([vp, C.c_int], C.c_int),
         "mf_ik_batch": ([vp, C.c_int, dp, dp, dp, dp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double], C.c_int),
         "mf_ik_batch_dev": ([vp, C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, vp],
                             C.c_int),
@@ -144,7 +143,7 @@ EXPORTED_SYMBOLS = [
     "mf_id", "mf_fk", "mf_jac", "mf_id_dev", "mf_fk_dev", "mf_jac_dev", "mf_problem_create", "mf_problem_free",
     "mf_problem_wsize", "mf_node_eval", "mf_solve_batch", "mf_solve_batch_dev", "mf_solve_batch_ws",
     "mf_solve_batch_ws_dev", "mf_problem_timing",
-    "mf_problem_kernel_stats", "mf_problem_trace", "mf_kernel_name", "mf_problem_kkt_lanes", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
+    "mf_problem_kernel_stats", "mf_problem_trace", "mf_kernel_name", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
     "mf_gproblem_create", "mf_gproblem_free", "mf_gproblem_dims", "mf_gsolve_batch", "mf_gsolve_batch_dev",
     "mf_gnode_record", "mf_gdebug_duals",
 ]

@@ -85,30 +85,6 @@ __device__ __forceinline__ void wave_lds_sync() { __asm__ volatile("s_waitcnt lg
 // all of the wave's memory operations (global stores read back by other lanes, LDS) complete
 __device__ __forceinline__ void wave_mem_sync() { __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
-
-// W-lane segments of the wave (W = 64: the whole wave; W = 32: two horizons per wave, one per half).
-// seg_lane: this lane's index within its segment; seg_readlane_d: lane l of this lane's own segment
-// (v_readlane ignores EXEC, so both halves are read and each lane keeps its own half's value).
-template <int W> __device__ __forceinline__ int seg_lane() {
-    static_assert(W == 64 || W == 32, "segments of 64 or 32 lanes");
-    if constexpr (W == 64) return lane_opaque();
-    else return lane_opaque() & (W - 1);
-}
-template <int W> __device__ __forceinline__ double seg_readlane_d(double v, int l) {
-    if constexpr (W == 64) {
-        return readlane_d(v, l);
-    } else {
-        const double v0 = readlane_d(v, l), v1 = readlane_d(v, 32 + l);
-        return (threadIdx.x & 32) ? v1 : v0;
-    }
-}
-
-
 struct BKInertia {
     int pos, neg, zero;
 };
@@ -222,9 +198,9 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
 
 // Same factorisation with a compile-time size M <= 64: the pivot scans are unrolled, so their
 // LDS reads issue back to back instead of one dependent round trip per candidate.
-template <int LD, int M, int W = 64>
+template <int LD, int M>
 __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
-    const int lane = seg_lane<W>();
+    const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     BKInertia in{0, 0, 0};
     if (lane < M) perm[lane] = lane;
@@ -272,11 +248,11 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
         int kk = k + kstep - 1;
         if (kp != kk) {
             wave_lds_sync();
-            for (int j = lane; j < M; j += W) {
+            for (int j = lane; j < M; j += 64) {
                 double t = A[kk * LD + j]; A[kk * LD + j] = A[kp * LD + j]; A[kp * LD + j] = t;
             }
             wave_lds_sync();
-            for (int i = lane; i < M; i += W) {
+            for (int i = lane; i < M; i += 64) {
                 double t = A[i * LD + kk]; A[i * LD + kk] = A[i * LD + kp]; A[i * LD + kp] = t;
             }
             if (lane == 0) { int t = perm[kk]; perm[kk] = perm[kp]; perm[kp] = t; }
@@ -287,7 +263,7 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
             if (d > 0) in.pos++; else if (d < 0) in.neg++; else in.zero++;
             const double inv = 1.0 / d;
             const int t = M - k - 1;
-            for (int e = lane; e < t * t; e += W) {
+            for (int e = lane; e < t * t; e += 64) {
                 const int i = k + 1 + e / t, j = k + 1 + e % t;
                 if (j <= i) {
                     const double ci = A[i * LD + k], cj = A[j * LD + k];
@@ -297,7 +273,7 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
                 }
             }
             wave_lds_sync();
-            for (int i = k + 1 + lane; i < M; i += W) {
+            for (int i = k + 1 + lane; i < M; i += 64) {
                 const double l = A[i * LD + k] * inv;
                 A[i * LD + k] = l;
                 A[k * LD + i] = l;
@@ -311,7 +287,7 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
             else in.zero += 2;
             const double ia = c / det, ib = -bb / det, ic = a / det;
             const int t = M - k - 2;
-            for (int e = lane; e < t * t; e += W) {
+            for (int e = lane; e < t * t; e += 64) {
                 const int i = k + 2 + e / t, j = k + 2 + e % t;
                 if (j <= i) {
                     const double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
@@ -323,7 +299,7 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
                 }
             }
             wave_lds_sync();
-            for (int i = k + 2 + lane; i < M; i += W) {
+            for (int i = k + 2 + lane; i < M; i += 64) {
                 const double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
                 A[i * LD + k] = c0i * ia + c1i * ib;
                 A[i * LD + k + 1] = c0i * ib + c1i * ic;
@@ -336,6 +312,12 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
     return in;
 }
 
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
 // Fast path for the stage block K = [[Q, D^T], [D, -dc]] (M = MU + ML, ML <= 2) in registers.
 // Lane i keeps row i of K (symmetric) and row i of the right-hand sides B (M x NR in LDS,
 // nr <= NR columns).  Q is eliminated by LDL^T with 1x1 pivots in natural order, each pivot
@@ -346,12 +328,11 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
 // inertia(S), so the inertia test is the same exact test as a pivoted factorisation of K.
 // On success the solution overwrites B; if a pivot fails the test (or S is singular) it
 // returns false with A and B untouched and the caller runs the pivoted LDS path.
-template <int LD, int NR, int MU, int ML, int W = 64>
+template <int LD, int NR, int MU, int ML>
 __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in) {
     constexpr int M = MU + ML;
     static_assert(ML <= 2, "Schur block of at most 2 rows");
-    static_assert(M <= W, "one lane per row within the segment");
-    const int lane = seg_lane<W>();
+    const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     double a[M], y[NR];
 #pragma unroll
@@ -365,8 +346,8 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
         if (ok) {
             double colmax = 0.0;
 #pragma unroll
-            for (int i = k + 1; i < MU; i++) colmax = fmax(colmax, fabs(seg_readlane_d<W>(a[k], i)));
-            const double d = seg_readlane_d<W>(a[k], k);
+            for (int i = k + 1; i < MU; i++) colmax = fmax(colmax, fabs(readlane_d(a[k], i)));
+            const double d = readlane_d(a[k], k);
             if (!(fabs(d) >= alpha * colmax) || d == 0.0) {
                 ok = false;
             } else {
@@ -374,9 +355,9 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
                 const double inv = 1.0 / d;
                 double r[M], yk[NR];
 #pragma unroll
-                for (int j = k + 1; j < M; j++) r[j] = seg_readlane_d<W>(a[j], k);
+                for (int j = k + 1; j < M; j++) r[j] = readlane_d(a[j], k);
 #pragma unroll
-                for (int c = 0; c < NR; c++) yk[c] = seg_readlane_d<W>(y[c], k);
+                for (int c = 0; c < NR; c++) yk[c] = readlane_d(y[c], k);
                 if (lane > k && lane < M) {
                     const double l = a[k] * inv;
 #pragma unroll
@@ -391,14 +372,14 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
     if (!ok) return false;
     // Schur block: inertia and x_S = S^{-1} y_S (rows MU..M-1)
     if (ML == 1) {
-        const double s00 = seg_readlane_d<W>(a[MU], MU);
+        const double s00 = readlane_d(a[MU], MU);
         if (s00 == 0.0) return false;
         if (s00 > 0) pos++; else neg++;
         if (lane == MU)
 #pragma unroll
             for (int c = 0; c < NR; c++) y[c] = y[c] / s00;
     } else if (ML == 2) {
-        const double s00 = seg_readlane_d<W>(a[MU], MU), s01 = seg_readlane_d<W>(a[MU + 1], MU), s11 = seg_readlane_d<W>(a[M - 1], M - 1);
+        const double s00 = readlane_d(a[MU], MU), s01 = readlane_d(a[MU + 1], MU), s11 = readlane_d(a[M - 1], M - 1);
         const double det = s00 * s11 - s01 * s01;
         if (det == 0.0) return false;
         if (det < 0) { pos++; neg++; }
@@ -406,7 +387,7 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
         else neg += 2;
         double y0[NR], y1[NR];
 #pragma unroll
-        for (int c = 0; c < NR; c++) { y0[c] = seg_readlane_d<W>(y[c], MU); y1[c] = seg_readlane_d<W>(y[c], M - 1); }
+        for (int c = 0; c < NR; c++) { y0[c] = readlane_d(y[c], MU); y1[c] = readlane_d(y[c], M - 1); }
         if (lane == MU)
 #pragma unroll
             for (int c = 0; c < NR; c++) y[c] = (s11 * y0[c] - s01 * y1[c]) / det;
@@ -427,7 +408,7 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
     for (int i = M - 1; i > 0; i--) {
         double xi[NR];
 #pragma unroll
-        for (int c = 0; c < NR; c++) xi[c] = seg_readlane_d<W>(y[c], i);
+        for (int c = 0; c < NR; c++) xi[c] = readlane_d(y[c], i);
         if (lane < i && lane < MU) {
             const double lit = a[i] * dinv;
 #pragma unroll
@@ -449,9 +430,9 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
 // of B (m x NR row-major in LDS) in registers and runs both triangular sweeps itself, reading
 // the factor by LDS broadcast; no cross-lane traffic and a single barrier.  The L column t
 // acts on rows >= t + 1, or >= t + 2 when t opens a 2x2 pivot (its partner row belongs to D).
-template <int LD, int NR, int M, int W = 64>
+template <int LD, int NR, int M>
 __device__ void bk_solve_cols(const double *A, const int *perm, const int *piv, double *B, int nr) {
-    const int c = seg_lane<W>();
+    const int c = lane_opaque();
     double y[M];
     int pv[M];
     if (c < nr) {

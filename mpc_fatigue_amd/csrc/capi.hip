@@ -517,7 +517,6 @@ extern "C" int mf_problem_create(const mf_model *mc, const mf_problem_spec *spec
     memcpy(C.qd_hi, spec->qd_hi, sizeof C.qd_hi);
     memcpy(C.q_lo, spec->q_lo, sizeof C.q_lo);
     memcpy(C.q_hi, spec->q_hi, sizeof C.q_hi);
-    C.kkt_lanes = 32;
     *out = p;
     return MF_OK;
 }
@@ -827,14 +826,6 @@ extern "C" int mf_problem_timing(mf_problem *p, int enable) {
     p->timing = enable ? 1 : 0;
     for (int k = 0; k < MF_NKERNELS; k++) { p->t_ms[k] = 0; p->t_launch[k] = 0; }
     return MF_OK;
-}
-
-extern "C" int mf_problem_kkt_lanes(mf_problem *p, int lanes) {
-    if (!p) return fail(MF_ERR_ARG, "null problem");
-    if (lanes == 0) return p->C.kkt_lanes;
-    if (lanes != 32 && lanes != 64) return fail(MF_ERR_ARG, "kkt lanes must be 32 or 64");
-    p->C.kkt_lanes = lanes;
-    return lanes;
 }
 
 extern "C" const char *mf_kernel_name(int slot) {

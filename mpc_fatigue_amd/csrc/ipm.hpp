@@ -36,7 +36,6 @@ struct OcpConst {
     double tol, constr_viol_tol, mu_init, F_init;
     int max_iter;
     int warm_start;        // IPOPT warm_start_init_point constants for a w0 start (k_ipm_init)
-    int kkt_lanes;         // k_ipm_kkt lanes per horizon: 32 (two horizons per wavefront) or 64
 };
 
 // Device arrays; every per-problem array is [batch][size] with the size below.

@@ -1366,21 +1366,9 @@ __global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, in
     }
 }
 
-#ifndef MF_KKT32_WAVES
-#define MF_KKT32_WAVES 2
-#endif
-// W = 64: one horizon per wavefront; W = 32: two horizons per wavefront, one per 32-lane half.  Every
-// stage role uses at most 27 lanes (the stage block, 9 x 9 entries of a 13 x 13 Hessian excepted: those
-// loop), so a half carries a horizon's recursion with the same instructions, in the same order, as a
-// whole wave: the two halves' stages issue together (the serial chain is FP64-issue bound, most
-// instructions using 6, 7 or 25 lanes).  Divergent decisions (pivots, inertia retries, the null-space
-// or pivoted path) run under EXEC masks; nothing here is a workgroup barrier after the model staging.
-template <int NJ, int NF, int NL, int W>
-__global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(const DevModel *__restrict__ Mg,
-                                                                  const DevFrame *__restrict__ Fg, OcpConst C,
-                                                                  IpmArrays A, int batch) {
-    static_assert(W == 64 || W == 32, "a horizon per wave or per half wave");
-    constexpr int HPW = 64 / W;  // horizons per wavefront
+template <int NJ, int NF, int NL>
+__global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+                                                 OcpConst C, IpmArrays A, int batch) {
     constexpr int n = NJ, nf = NF, nl = NL;
     constexpr int NV = 2 * NJ + NF;
     constexpr int NFA = NF > 0 ? NF : 1;
@@ -1389,35 +1377,22 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
     __shared__ ModelLds<NJ> Ml;
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
-    __shared__ int perm_[HPW][MB], piv_[HPW][MB];
-    const int nrun = *A.nrun;
-    const int hf = (W == 64) ? 0 : (int)(threadIdx.x >> 5);  // horizon slot of this lane within the wave
-    const int lane = (W == 64) ? (int)threadIdx.x : (int)(threadIdx.x & (W - 1));
-    const int slot = (int)blockIdx.x * HPW + hf;
-    if ((int)blockIdx.x * HPW >= nrun) return;
-    const int b = A.list[min(slot, nrun - 1)];
+    __shared__ int perm[MB], piv[MB];
+    const int lane = threadIdx.x;
+    if ((int)blockIdx.x >= *A.nrun) return;
+    const int b = A.list[blockIdx.x];
     ProbState st = A.st[b];
-    const bool live = slot < nrun && st.status == ST_RUNNING;
-    if constexpr (W == 64) {
-        if (!live) return;
-    } else {
-        if (!__any(live)) return;  // the wave stages the model for both halves before either leaves
-    }
-    int *perm = perm_[hf], *piv = piv_[hf];
+    if (st.status != ST_RUNNING) return;
     Ml.load(Mg);
     stage_lds(&F, Fg);
     __shared__ double Bnd[4 * NJ];  // q_lo, q_hi, qd_lo, qd_hi (kernel-argument arrays read per element)
-    if (threadIdx.x < NJ) {
-        const int j = threadIdx.x;
-        Bnd[j] = C.q_lo[j];
-        Bnd[NJ + j] = C.q_hi[j];
-        Bnd[2 * NJ + j] = C.qd_lo[j];
-        Bnd[3 * NJ + j] = C.qd_hi[j];
+    if (lane < NJ) {
+        Bnd[lane] = C.q_lo[lane];
+        Bnd[NJ + lane] = C.q_hi[lane];
+        Bnd[2 * NJ + lane] = C.qd_lo[lane];
+        Bnd[3 * NJ + lane] = C.qd_hi[lane];
     }
     __syncthreads();
-    if constexpr (W != 64) {
-        if (!live) return;  // an empty or finished half leaves; its partner runs alone
-    }
     STAMP_INIT;
 
     const IpmSizes S = ipm_sizes(C);
@@ -1432,24 +1407,11 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
     double *dzqL = A.dzqL + b * S.q, *dzqU = A.dzqU + b * S.q, *dzdL = A.dzdL + b * S.u, *dzdU = A.dzdU + b * S.u;
     double *dvL = A.dvL + b * S.u, *dvU = A.dvU + b * S.u;
     const double *tau = A.tau + b * S.u, *Jt = A.Jt + b * S.jt, *line = A.line + b * S.l, *Jl = A.Jl + b * S.jl;
-    const double *Wh = A.W + b * S.w, *gf = A.gf + b * S.gf, *cost = A.cost + b * S.cost;
+    const double *W = A.W + b * S.w, *gf = A.gf + b * S.gf, *cost = A.cost + b * S.cost;
     double *Sxq = A.Sxq + b * S.q, *gphq = A.gphq + b * S.q, *Sxd = A.Sxd + b * S.u, *gphd = A.gphd + b * S.u;
     double *Ss = A.Ss + b * S.u, *gphs = A.gphs + b * S.u;
     double *G = A.G + b * S.G, *wv = A.wv + b * S.wv;
     const double *lref = A.lref + b * 2;
-    // Per-horizon bases used inside the serial loops are recomputed at each use from an opaque copy of b:
-    // with W = 32 the two halves hold different horizons, b lives in a VGPR and every base held across
-    // the stage loop would cost two VGPRs (W = 64: b is uniform and the bases stay scalar, as before).
-    auto bo = [&]() -> size_t {
-        if constexpr (W == 64) {
-            return (size_t)b;
-        } else {
-            int v = b;
-            __asm__ volatile("" : "+v"(v));
-            return (size_t)v;
-        }
-    };
-#define HB(arr, sz) (A.arr + bo() * S.sz)
     const double *tlo = A.tau_lo, *thi = A.tau_hi;
     const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
 #define TACT(k, j) (hasb(tlo[(k) * n + (j)]) || hasb(thi[(k) * n + (j)]))
@@ -1461,8 +1423,8 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
     auto finish = [&](int status) {
         STAMP_FLUSH;
         double f = 0.0;
-        for (int k = lane; k < N; k += W) f += HB(cost, cost)[k];
-        f = hw_sum<W>(f);
+        for (int k = lane; k < N; k += 64) f += cost[k];
+        f = wave_sum(f);
         if (lane == 0) {
             st.status = status;
             st.obj = f;
@@ -1491,40 +1453,32 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
     constexpr int NRK = NJ + 1;
     constexpr int NLA2 = NL > 0 ? NL : 1;
     constexpr int NVV = NV * NV;
-    constexpr int NHR = (NVV + W - 1) / W;   // H entries per lane
+    constexpr int NHR = (NVV + 63) / 64;     // H entries per lane
     // H0 is stored as its lower triangle (k_eval_asm): lane entry e = (u, v) reads (max, min)
     int hlo[NHR];
 #pragma unroll
     for (int t = 0; t < NHR; t++) {
-        const int e = min(lane + W * t, NVV - 1), u = e / NV, v = e % NV;
+        const int e = min(lane + 64 * t, NVV - 1), u = e / NV, v = e % NV;
         hlo[t] = u >= v ? e : v * NV + u;
     }
     constexpr int SLOT = MB * NJ + MB;       // Riccati slot (G_k | wv_k) doubles
+    __shared__ double Hs[NVV];
+    __shared__ double Ps[NJ * NJ], ps[NJ], ss[NJ], Pn[NJ * (NJ + 1)];
+    __shared__ double Ks[NK * LDK], Rk[NK * NRK];
+    __shared__ double Gl[NLA2 * NJ];
     constexpr int NRS = NU > 2 ? NU - 2 : 1;
-    // per-horizon LDS of the recursion (one block per horizon of the wave)
-    struct Lds {
-        double Hs[NVV];
-        double Ps[NJ * NJ], ps[NJ], ss[NJ], Pn[NJ * (NJ + 1)];
-        double Ks[NK * LDK], Rk[NK * NRK];
-        double Gl[NLA2 * NJ];
-        double Ss5[NRS * NRS + 4 * NRS + 3];  // reduced Hessian + tables (stage_ns.hpp)
-        double Jl_s[NJ * NV];                 // J_k (torque Jacobian) of the stage, regularised tries only
-        double Stg[NV + 2 * NJ + NLA2];       // stage k's block, staged from a register prefetch
-    };
-    __shared__ Lds L_[HPW];
-    Lds &Lh = L_[hf];
-    double *Hs = Lh.Hs, *Ps = Lh.Ps, *ps = Lh.ps, *ss = Lh.ss, *Pn = Lh.Pn, *Ks = Lh.Ks, *Rk = Lh.Rk, *Gl = Lh.Gl;
-    double *Ss5 = Lh.Ss5, *Jl_s = Lh.Jl_s;
+    __shared__ double Ss5[NRS * NRS + 4 * NRS + 3];  // reduced Hessian + tables (stage_ns.hpp)
+    __shared__ double Jl_s[NJ * NV];  // J_k (torque Jacobian) of the stage, regularised tries only
     // per-stage inputs of the recursion, computed for all stages at once by the whole wave (global
     // scratch, stage k contiguous): g_k (NV), c_k = q_k + h qd_k - q_{k+1} (NJ),
     // e_k = line_{k+1} + Jl_{k+1} c_k (NLA2), dD_k = D_tau(dw, dc) - Sigma_s (NJ); then
     // y_tau + D_tau r_tau (N x NJ, used inside prep only)
     constexpr int SG = NV + 2 * NJ + NLA2;
     double *stg = A.stg + b * S.stg;
-    double *wst = HB(stg, stg) + (size_t)N * SG;
-    double *Stg = Lh.Stg;
+    double *wst = stg + (size_t)N * SG;
+    __shared__ double Stg[SG];  // stage k's block, staged from a register prefetch
     auto prep_stages = [&](double dwv, double dcv) {
-        prep_stage_inputs<NJ, NF, NL, W>(C, A, b, lane, dwv, dcv, [] { wave_mem_sync(); });
+        prep_stage_inputs<NJ, NF, NL, 64>(C, A, b, lane, dwv, dcv, [] { wave_mem_sync(); });
     };
     double dw, dc = 0.0, dFr, reg;
     const int reg_tier0 = st.reg_tier;
@@ -1545,32 +1499,32 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
         const bool dreg = (dw != 0.0 || dc != 0.0);
         const bool dgreg = (dw != 0.0 || dFr != 0.0);  // diagonal regularisation of H
         // terminal value function V_N = 1/2 x^T P x + p^T x
-        for (int e = lane; e < n * n; e += W) {
+        for (int e = lane; e < n * n; e += 64) {
             int i = e / n, j = e % n;
-            Ps[e] = (i == j) ? HB(Sxq, q)[N * n + i] + dw : 0.0;
+            Ps[e] = (i == j) ? Sxq[N * n + i] + dw : 0.0;
         }
-        for (int j = lane; j < n; j += W) ps[j] = HB(gphq, q)[N * n + j] - HB(yc, u)[(N - 1) * n + j];
+        for (int j = lane; j < n; j += 64) ps[j] = gphq[N * n + j] - yc[(N - 1) * n + j];
         // prefetch H0_{N-1} (and J_{N-1} when the torque block is regularised)
-        constexpr int NJV = NJ * NV, NJR = (NJV + W - 1) / W;
+        constexpr int NJV = NJ * NV, NJR = (NJV + 63) / 64;
         double hr[NHR], jr[NJR];
 #pragma unroll
         for (int t = 0; t < NHR; t++) {
-            const int e = lane + W * t;
-            hr[t] = (e < NVV) ? HB(W, w)[(size_t)(N - 1) * NVV + hlo[t]] : 0.0;
+            const int e = lane + 64 * t;
+            hr[t] = (e < NVV) ? W[(size_t)(N - 1) * NVV + hlo[t]] : 0.0;
         }
 #pragma unroll
         for (int t = 0; t < NJR; t++) {
-            const int e = lane + W * t;
-            jr[t] = (dreg && e < NJV) ? HB(Jt, jt)[(size_t)(N - 1) * NJV + e] : 0.0;
+            const int e = lane + 64 * t;
+            jr[t] = (dreg && e < NJV) ? Jt[(size_t)(N - 1) * NJV + e] : 0.0;
         }
         double glr = 0.0;  // Jl_{k+1} entry of this lane for the next stage
-        double sgr = (lane < SG) ? HB(stg, stg)[(size_t)(N - 1) * SG + lane] : 0.0;  // stage block, one ahead
+        double sgr = (lane < SG) ? stg[(size_t)(N - 1) * SG + lane] : 0.0;  // stage block, one ahead
         // block row of Rk holding slot row c (slot rows in control order: qd 0..n-1, F, then the
         // NL line multipliers)
         auto brow = [&](int c) { return c < NU ? (c < NJ ? NF + c : c - NJ) : c; };
         wave_lds_sync();
         for (int k = N - 1; k >= 0; k--) {
-            const int lane = seg_lane<W>();  // per-stage index arithmetic stays inside the stage
+            const int lane = lane_opaque();  // per-stage index arithmetic stays inside the stage
             // ---- H_k = H0_k (+ regularisation) into LDS; prefetch H0_{k-1}, Jl_k (, J_{k-1})
             STAMP(18);
             if (lane < SG) Stg[lane] = sgr;
@@ -1578,7 +1532,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             if (dreg) {
 #pragma unroll
                 for (int t = 0; t < NJR; t++) {
-                    const int e = lane + W * t;
+                    const int e = lane + 64 * t;
                     if (e < NJV) Jl_s[e] = jr[t];
                 }
                 wave_lds_sync();
@@ -1586,7 +1540,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             const double *dDk = Stg + NV + NJ + NLA2;
 #pragma unroll
             for (int t = 0; t < NHR; t++) {
-                const int e = lane + W * t;
+                const int e = lane + 64 * t;
                 if (e < NVV) {
                     const int u = e / NV, v = e % NV;
                     double a = hr[t];
@@ -1605,24 +1559,24 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             // put a full store round trip on the path of the next stage; issued here, they
             // complete behind the stage's own work.  P_{k+1}, p_{k+1} (slot k) are in Ps / ps;
             // stage k+1's Ku, Kl, ku, kl (slot k+1) are still in Rk.
-            double *Gk = HB(G, G) + (size_t)k * MB * n, *wk = HB(wv, wv) + (size_t)k * MB;
+            double *Gk = G + (size_t)k * MB * n, *wk = wv + (size_t)k * MB;
             if (lane < n) wk[NU + NL + lane] = ps[lane];
-            for (int e = lane; e < n * n; e += W) Gk[(NU + NL) * n + e] = Ps[e];
+            for (int e = lane; e < n * n; e += 64) Gk[(NU + NL) * n + e] = Ps[e];
             if (k + 1 < N) {
-                double *G1 = HB(G, G) + (size_t)(k + 1) * MB * n, *w1 = HB(wv, wv) + (size_t)(k + 1) * MB;
-                for (int e = lane; e < NK * n; e += W) G1[e] = Rk[brow(e / n) * NRK + e % n];  // Ku (NU x n), Kl (NL x n)
+                double *G1 = G + (size_t)(k + 1) * MB * n, *w1 = wv + (size_t)(k + 1) * MB;
+                for (int e = lane; e < NK * n; e += 64) G1[e] = Rk[brow(e / n) * NRK + e % n];  // Ku (NU x n), Kl (NL x n)
                 if (lane < NK) w1[lane] = Rk[brow(lane) * NRK + n];                             // ku, kl
             }
             if (k > 0) {
                 // unconditional loads from clamped addresses (a load whose value is selected
                 // against a constant is waited for on the spot)
 #pragma unroll
-                for (int t = 0; t < NHR; t++) hr[t] = HB(W, w)[(size_t)(k - 1) * NVV + hlo[t]];
-                if constexpr (NL > 0) glr = HB(Jl, jl)[(size_t)k * nl * n + min(lane, nl * n - 1)];
-                sgr = HB(stg, stg)[(size_t)(k - 1) * SG + min(lane, SG - 1)];
+                for (int t = 0; t < NHR; t++) hr[t] = W[(size_t)(k - 1) * NVV + hlo[t]];
+                if constexpr (NL > 0) glr = Jl[(size_t)k * nl * n + min(lane, nl * n - 1)];
+                sgr = stg[(size_t)(k - 1) * SG + min(lane, SG - 1)];
                 if (dreg)
 #pragma unroll
-                    for (int t = 0; t < NJR; t++) jr[t] = HB(Jt, jt)[(size_t)(k - 1) * NJV + min(lane + W * t, NJV - 1)];
+                    for (int t = 0; t < NJR; t++) jr[t] = Jt[(size_t)(k - 1) * NJV + min(lane + 64 * t, NJV - 1)];
             }
             // s = P c + p
             const double *ck = Stg + NV;
@@ -1639,14 +1593,14 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             if (k == 0) {
                 // only dF_0 is free (q_0, qd_0 fixed; the stage-1 line constraint is masked)
                 if (nf > 0) {
-                    for (int e = lane; e < nf * nf; e += W) Ks[(e / nf) * LDK + e % nf] = Hs[(2 * n + e / nf) * NV + 2 * n + e % nf];
-                    for (int a = lane; a < nf; a += W) Rk[a * NRK] = -gsk[2 * n + a];
+                    for (int e = lane; e < nf * nf; e += 64) Ks[(e / nf) * LDK + e % nf] = Hs[(2 * n + e / nf) * NV + 2 * n + e % nf];
+                    for (int a = lane; a < nf; a += 64) Rk[a * NRK] = -gsk[2 * n + a];
                     wave_lds_sync();
-                    BKInertia in = bk_factor_fixed<LDK, NFA, W>(Ks, perm, piv);
+                    BKInertia in = bk_factor_fixed<LDK, NFA>(Ks, perm, piv);
                     if (in.zero) { ok = false; zero = true; break; }
                     if (in.pos != nf) { ok = false; break; }
-                    bk_solve_cols<LDK, NRK, NFA, W>(Ks, perm, piv, Rk, 1);
-                    for (int a = lane; a < nf; a += W) wk[NJ + a] = Rk[a * NRK];  // dF_0 (ku slot)
+                    bk_solve_cols<LDK, NRK, NFA>(Ks, perm, piv, Rk, 1);
+                    for (int a = lane; a < nf; a += 64) wk[NJ + a] = Rk[a * NRK];  // dF_0 (ku slot)
                 }
                 wave_lds_sync();
                 break;
@@ -1658,7 +1612,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             auto uo = [&](int a) { return a < NF ? NJ + a : a - NF; };
             int nsr = -1;
             if constexpr (NL == 2) {
-                if (con && dc == 0.0) nsr = stage_nullspace<NJ, NF, NV, NRK, W>(Hs, Ps, ss, Gl, gsk, elk, h, Ss5, Rk);
+                if (con && dc == 0.0) nsr = stage_nullspace<NJ, NF, NV, NRK>(Hs, Ps, ss, Gl, gsk, elk, h, Ss5, Rk);
             }
             STAMP(13);
             STAMP_COUNT(17, 1);
@@ -1670,7 +1624,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
                 // carries the large curvature Sigma_s (J^T F)^2 and the joint velocities couple to it
                 // weakly, so natural-order 1x1 pivots pass the Bunch-Kaufman test (ldl_schur_regs).
                 // uo(a): control index (qd 0..n-1, F n..) of block row a < NU.
-                for (int e = lane; e < NK * NK; e += W) {
+                for (int e = lane; e < NK * NK; e += 64) {
                     int a = e / NK, c = e % NK;
                     double val;
                     if (a < NU && c < NU) {
@@ -1685,7 +1639,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
                     }
                     Ks[a * LDK + c] = val;
                 }
-                for (int e = lane; e < NK * NRK; e += W) {
+                for (int e = lane; e < NK * NRK; e += 64) {
                     int a = e / NRK, c = e % NRK;
                     double val;
                     if (a < NU) {
@@ -1701,21 +1655,21 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
                 wave_lds_sync();
                 STAMP(12);
                 BKInertia in;
-                const bool fast = ldl_schur_regs<LDK, NRK, NU, NL, W>(Ks, Rk, NRK, in);
+                const bool fast = ldl_schur_regs<LDK, NRK, NU, NL>(Ks, Rk, NRK, in);
                 STAMP(13);
                 if (fast) {
                     if (in.pos != NU || in.neg != NL) { ok = false; break; }
                 } else {
-                    in = bk_factor_fixed<LDK, NK, W>(Ks, perm, piv);
+                    in = bk_factor_fixed<LDK, NK>(Ks, perm, piv);
                     if (in.zero) { ok = false; zero = true; break; }
                     if (in.pos != NU || in.neg != NL) { ok = false; break; }
-                    bk_solve_cols<LDK, NRK, NK, W>(Ks, perm, piv, Rk, NRK);
+                    bk_solve_cols<LDK, NRK, NK>(Ks, perm, piv, Rk, NRK);
                 }
             }
             STAMP(14);
             // ---- P_k = Qxx + Qxu Ku + G^T Kl ; p_k = qx + Qxu ku + G^T kl   (block row a <-> control uo(a))
             // one pass over the n x (n + 1) entries [P_k | p_k] (column n of Rk holds ku, kl)
-            for (int e = lane; e < n * (n + 1); e += W) {
+            for (int e = lane; e < n * (n + 1); e += 64) {
                 const int i = e / (n + 1), j = e % (n + 1);
                 double a = (j < n) ? Hs[i * NV + j] + Ps[i * n + j] : gsk[i] + ss[i];
                 for (int r = 0; r < NU; r++) {
@@ -1728,7 +1682,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             }
             // (Ku, Kl, ku, kl stay in Rk: the next stage stores them, see the slot stores)
             wave_lds_sync();
-            for (int e = lane; e < n * n; e += W) {
+            for (int e = lane; e < n * n; e += 64) {
                 int i = e / n, j = e % n;
                 Ps[e] = 0.5 * (Pn[i * (n + 1) + j] + Pn[j * (n + 1) + i]);
             }
@@ -1774,7 +1728,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
     const int ra = min(lane, NK - 1);  // slot row of this lane: qd 0..n-1, F, then the line multipliers
     double rowr[FD][NJ], wkr[FD], ckr[FD];
     auto fetch = [&](int kk, double *row, double &wk, double &ck) {
-        const double *src = HB(G, G) + (size_t)kk * MB * n + (size_t)ra * n;
+        const double *src = G + (size_t)kk * MB * n + (size_t)ra * n;
         if constexpr (NJ % 2 == 0) {
             const double2 *s2 = reinterpret_cast<const double2 *>(src);  // 16-byte aligned: MB n, n even
 #pragma unroll
@@ -1787,16 +1741,16 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
 #pragma unroll
             for (int i = 0; i < NJ; i++) row[i] = src[i];
         }
-        wk = HB(wv, wv)[(size_t)kk * MB + ra];
-        ck = HB(stg, stg)[(size_t)kk * SG + NV + min(lane, NJ - 1)];
+        wk = wv[(size_t)kk * MB + ra];
+        ck = stg[(size_t)kk * SG + NV + min(lane, NJ - 1)];
     };
 #pragma unroll
     for (int r = 0; r < FD; r++) fetch(min(r, N - 1), rowr[r], wkr[r], ckr[r]);
     double xsv[NJ];  // dx_k, the same in every lane
 #pragma unroll
-    for (int j = 0; j < NJ; j++) xsv[j] = HB(stg, stg)[NV + j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
-    for (int j = lane; j < n; j += W) { HB(dq, q)[j] = 0.0; HB(dqd, u)[j] = 0.0; }
-    for (int l = lane; l < nl; l += W) { HB(dyl, l)[l] = 0.0; HB(dyl, l)[nl + l] = 0.0; }
+    for (int j = 0; j < NJ; j++) xsv[j] = stg[NV + j];  // dx_1 = c_0 (dx_0 = 0, dqd_0 = 0)
+    for (int j = lane; j < n; j += 64) { dq[j] = 0.0; dqd[j] = 0.0; }
+    for (int l = lane; l < nl; l += 64) { dyl[l] = 0.0; dyl[nl + l] = 0.0; }
     for (int k0 = 0; k0 < N; k0 += FD) {
 #pragma unroll
         for (int r = 0; r < FD; r++) {
@@ -1807,7 +1761,7 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             for (int i = 0; i < NJ; i++) row[i] = rowr[r][i];
             fetch(min(k + FD, N - 1), rowr[r], wkr[r], ckr[r]);  // past the end: slot N-1 again, unused
             if (k == 0) {  // only dF_0 is free; it sits in the ku slot of stage 0
-                if (lane >= NJ && lane < NU) HB(dF, f)[lane - NJ] = wk;
+                if (lane >= NJ && lane < NU) dF[lane - NJ] = wk;
                 continue;
             }
             double us = wk;
@@ -1819,18 +1773,18 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
             for (int j = 1; j < NJ; j++) xj = (lane == j) ? xsv[j] : xj;
             const double cs = xj + h * us + ck;  // dx_{k+1}, entry `lane` (lanes < n)
             if (lane < n) {
-                HB(dq, q)[k * n + lane] = xj;
-                HB(dqd, u)[k * n + lane] = us;
+                dq[k * n + lane] = xj;
+                dqd[k * n + lane] = us;
             } else if (lane < NU) {
-                HB(dF, f)[k * NFA + lane - NJ] = us;
+                dF[k * NFA + lane - NJ] = us;
             } else if (lane < NK) {
-                if (k + 1 < N) HB(dyl, l)[(k + 1) * nl + lane - NU] = con1 ? us : 0.0;
+                if (k + 1 < N) dyl[(k + 1) * nl + lane - NU] = con1 ? us : 0.0;
             }
 #pragma unroll
-            for (int j = 0; j < NJ; j++) xsv[j] = seg_readlane_d<W>(cs, j);
+            for (int j = 0; j < NJ; j++) xsv[j] = readlane_d(cs, j);
         }
     }
-    for (int j = lane; j < n; j += W) HB(dq, q)[N * n + j] = xsv[j];
+    for (int j = lane; j < n; j += 64) dq[N * n + j] = xsv[j];
     // dyc, dyd, ds, the bound multiplier steps and pcorr: k_kkt_recover (a block per horizon)
     STAMP(3);
     STAMP_FLUSH;
@@ -1839,7 +1793,6 @@ __global__ __launch_bounds__(64, (W == 64 ? 3 : MF_KKT32_WAVES)) void k_ipm_kkt(
         st.kkt_dc = dc;
         A.st[b] = st;
     }
-#undef HB
 #undef TACT
 }
 
@@ -2243,10 +2196,7 @@ struct IpmLaunch {
         } else if (phase == 2) {
             hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, M, F, C, A, batch);
         } else if (phase == 3) {
-            if (C.kkt_lanes == 32)  // two horizons per wavefront
-                hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL, 32>), dim3((nact + 1) / 2), dim3(64), 0, s, M, F, C, A, batch);
-            else
-                hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL, 64>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
+            hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
             hipLaunchKernelGGL((k_kkt_recover<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
         } else {
             hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);

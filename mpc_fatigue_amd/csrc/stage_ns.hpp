@@ -40,13 +40,12 @@ __device__ __forceinline__ double rcp_nr(double d) {
 
 // returns 1: solved, inertia (NU, 2); 0: wrong inertia; -1: degenerate (use the pivoted path).
 // Ss5: LDS scratch of NR * NR + 4 * NR + 3 doubles (reduced Hessian, then the Z / Q tables).
-template <int NJ, int NF, int NV, int NRK, int W = 64>
+template <int NJ, int NF, int NV, int NRK>
 __device__ __forceinline__ int stage_nullspace(const double *Hs, const double *Ps, const double *ss, const double *Gl,
                                                const double *gsk, const double *elk, double h, double *Ss5,
                                                double *Rk) {
     constexpr int NU = NJ + NF, NR = NU - 2;
-    static_assert(4 * NR + 3 <= W && NR * NR <= W && NRK <= W, "one table entry per lane of the segment");
-    const int lane = seg_lane<W>();
+    const int lane = lane_opaque();
     const double hh = h * h;
     // Q entry (controls x, y; x, y < NJ are joint velocities)
     auto Qe = [&](int x, int y) {

@@ -131,10 +131,6 @@ class OCP:
         _lib.check(_lib.lib().mf_solve_batch_dev(self._h, batch, q0_ptr, lref_ptr, C.byref(o), out["w"],
                                                  out["status"], out["iters"], out["kkt"], out["obj"], stream))
 
-    def kkt_lanes(self, lanes: int = 0) -> int:
-        """Lanes per horizon of the Riccati kernel: 32 (two horizons per wavefront) or 64; 0 queries."""
-        return _lib.check(_lib.lib().mf_problem_kkt_lanes(self._h, int(lanes)))
-
     def timing(self, enable: bool = True) -> None:
         _lib.check(_lib.lib().mf_problem_timing(self._h, int(enable)))
 

@@ -233,29 +233,6 @@ def test_reference_15nm_floor_same_nonconverged_status():
     assert r.cviol > 1.0 and res.kkt[0] > 1.0
 
 
-@pytest.mark.parametrize("B", [257, 1])
-def test_kkt_two_horizons_per_wave_bit_identical(B):
-    """k_ipm_kkt with two horizons per wavefront (32-lane halves, the default) runs each horizon's Riccati
-    recursion with the same arithmetic in the same order as one horizon per wavefront: every output of the
-    C5 batch is bit-identical between the two (an odd batch leaves the last wave's second half empty)."""
-    N = 100
-    base = PR.pilz6_bench(N=N)
-    ocp = OCP(base)
-    ref = load_urdf_file(PR.urdf_path(base["urdf"]))
-    Q0 = PR.pilz6_batch_q0(B, seed=0)
-    LR = np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in Q0])
-    kw = dict(line_ref=LR, F_init=PR.BENCH_F_INIT, tol=1e-8, constr_viol_tol=1e-8, max_iter=300)
-    assert ocp.kkt_lanes() == 32
-    r32 = ocp.solve(Q0, **kw)
-    ocp.kkt_lanes(64)
-    r64 = ocp.solve(Q0, **kw)
-    ocp.kkt_lanes(32)
-    assert (r32.status == 0).all() and (r64.status == 0).all()
-    np.testing.assert_array_equal(r32.iters, r64.iters)
-    np.testing.assert_array_equal(r32.w, r64.w)
-    np.testing.assert_array_equal(r32.kkt, r64.kkt)
-
-
 def test_first_solve_on_a_non_blocking_stream():
     """A fresh problem's first solve on a non-blocking (torch) stream: the workspace is zeroed on the
     solve's own stream, so the solve cannot race the zeroing (it once did: every horizon of the first

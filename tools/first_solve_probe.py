@@ -16,9 +16,8 @@ dev = torch.device("cuda", 0)
 spec = PR.pilz6_bench(N=100)
 opts = dict(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, F_init=PR.BENCH_F_INIT)
 Q0 = PR.pilz6_batch_q0(B, seed=0)
-for lanes, stream_kind in ((64, "default"), (32, "default"), (32, "own"), (64, "own")):
+for stream_kind in ("own", "default"):
     ocp = OCP(spec)
-    ocp.kkt_lanes(lanes)
     q0 = torch.tensor(Q0, dtype=torch.float64, device=dev)
     pos = torch.empty((B, 3), dtype=torch.float64, device=dev)
     st = torch.cuda.current_stream(dev) if stream_kind == "default" else torch.cuda.Stream(dev)
@@ -36,6 +35,6 @@ for lanes, stream_kind in ((64, "default"), (32, "default"), (32, "own"), (64, "
         torch.cuda.synchronize(dev)
         s = out["status"].cpu().numpy()
         it = out["iters"].cpu().numpy()
-        print(f"lanes {lanes} stream {stream_kind} solve {rep}: {time.perf_counter() - t:.2f}s conv {(s == 0).sum()} "
+        print(f"stream {stream_kind} solve {rep}: {time.perf_counter() - t:.2f}s conv {(s == 0).sum()} "
               f"status {np.bincount(s, minlength=4).tolist()} mean it {it.mean():.2f} max {it.max()}", flush=True)
     del ocp
