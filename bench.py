@@ -60,8 +60,8 @@ def cpu_threads() -> tuple[int, str]:
 def cpu_baseline(spec_of, Q0, lrefs, opts, threads: int, sample_mt: int, sample_1t: int, reps: int):
     """The CPU baseline (rank 0, N = 1): the same interior-point algorithm on the host -- the generic
     oracle IPM (oracle/mf_ocp.c) with the product's forward-over-reverse node functions compiled for
-    the host (oracle/cpu_fast.cpp, -O3 AVX2/FMA) -- OpenMP over horizons on `threads` cores and on one
-    core; median of `reps` timed runs after one warm-up run.  Also the phase split of the host solve
+    the host (oracle/cpu_fast.cpp, -O3 AVX2/FMA) and the device's Riccati KKT recursion -- OpenMP over
+    horizons on `threads` cores and on one core; median of `reps` timed runs after one warm-up run.  Also the phase split of the host solve
     (node derivatives / KKT factorisation / directions / line search, mfg_time_get).
     Returns (record, CPU solutions)."""
     import ctypes as C
@@ -69,7 +69,7 @@ def cpu_baseline(spec_of, Q0, lrefs, opts, threads: int, sample_mt: int, sample_
     from oracle import cpu_fast as CF
 
     specs = [spec_of(Q0[i], lrefs[i]) for i in range(max(sample_mt, sample_1t))]
-    kw = dict(opts, **CF.FastNodes(specs[0]).opts_kw())
+    kw = dict(opts, riccati=True, **CF.FastNodes(specs[0]).opts_kw())
     L = C.CDLL(CF.LIB)
     L.mfg_time_get.argtypes = [C.POINTER(C.c_double)]
 
@@ -103,8 +103,8 @@ def cpu_baseline(spec_of, Q0, lrefs, opts, threads: int, sample_mt: int, sample_
            "sample": (f"first {sample_mt} horizons of the same batch on {threads} threads and the first {sample_1t} "
                       f"on 1 thread (median of {reps} runs after a warm-up); generic IPM oracle/mf_ocp.c with the "
                       "product's node functions, both built for the host at -O3 -march=x86-64-v3 (oracle/libmfcpu.so); "
-                      "KKT by the block-tridiagonal Bunch-Kaufman factorisation (time_split_one_core gives its share; "
-                      "the GPU factors the same KKT by a Riccati recursion)")}
+                      "KKT by the device's Riccati recursion (mfg_opts.riccati, stage blocks factored by Bunch-Kaufman, "
+                      "the GPU's algorithm), not the checker's block-tridiagonal factorisation")}
     return rec, w_mt, st_mt
 
 

@@ -117,6 +117,10 @@ typedef struct {
      * given (CasADi's lam_g0 defaults to 0).  dual_in: optional multipliers in the dual_out layout. */
     int warm_start;
     const double *dual_in;
+    /* 1: factor the KKT by the Riccati recursion the device solver runs (csrc/gipm.hip: stage blocks
+     * [[Q_uu, D_u^T], [D_u, -dc]], Sylvester inertia per stage) instead of the block-tridiagonal
+     * Bunch-Kaufman factorisation; the same Newton direction up to round-off (the CPU baseline) */
+    int riccati;
 } mfg_opts;
 
 typedef struct {
@@ -311,6 +315,11 @@ typedef struct {
     /* constraint residuals: current point, trial point, second-order correction */
     double *rdyn, *rin, *req, *trdyn, *trin, *treq, *sdyn, *sin_, *seq;
     double *bk;                      /* saved direction (second-order corrections) */
+    /* Riccati factorisation (mfg_opts.riccati): P_{k+1} per stage, stage block factors, gains, and the
+     * vector pass's p_{k+1} / k_k */
+    int ric, nk;
+    double *Pg, *Kst, *Fg, *pvg, *kvg;
+    int *Kpp;
 } ws_t;
 
 /* per-problem data handed to the node callbacks: the line reference, or the Centauro pose targets
@@ -597,6 +606,45 @@ static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
     return (npos_t == want_pos && nneg_t == want_neg) ? 0 : 1;
 }
 
+/* the slack-row steps (dyi, ds) and the bound-multiplier steps of a primal-dual direction */
+static void slack_and_bound_steps(ws_t *S, double mu, const double *rin) {
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni;
+    const double dw = S->dw, dc = S->dc;
+    for (int k = 0; k < N; k++) {
+        const double *Ji = S->Ji + (size_t)k * ni * nv;
+        for (int q = 0; q < ni; q++) {
+            const int i = k * ni + q;
+            if (!CACT(S, k, q)) { S->dyi[i] = 0; S->ds[i] = 0; continue; }
+            double jd = 0;
+            for (int a = 0; a < nx; a++) jd += Ji[q * nv + a] * S->dx[k * nx + a];
+            for (int a = 0; a < nu; a++) jd += Ji[q * nv + nx + a] * S->du[k * nu + a];
+            const double sg = S->Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
+            const double rs = S->gs[i] - S->yi[i];
+            S->dyi[i] = Dd * (jd + rin[i] + rs / sg);
+            S->ds[i] = (S->dyi[i] - rs) / sg;
+        }
+    }
+#define DZ(dzl, dzu, zl, zu, v, dv, lo, hi)                                              \
+    do {                                                                                 \
+        dzl = dzu = 0;                                                                   \
+        if (hasb(lo)) dzl = mu / ((v) - (lo)) - (zl) - (zl) / ((v) - (lo)) * (dv);       \
+        if (hasb(hi)) dzu = mu / ((hi) - (v)) - (zu) + (zu) / ((hi) - (v)) * (dv);       \
+    } while (0)
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            if (k == 0) { S->dzxL[i] = S->dzxU[i] = 0; continue; }
+            DZ(S->dzxL[i], S->dzxU[i], S->zxL[i], S->zxU[i], S->x[i], S->dx[i], S->xlo[j], S->xhi[j]);
+        }
+    for (int i = 0; i < N * nu; i++) {
+        if (S->ufix[i]) { S->dzuL[i] = S->dzuU[i] = 0; continue; }
+        DZ(S->dzuL[i], S->dzuU[i], S->zuL[i], S->zuU[i], S->u[i], S->du[i], S->ulo[i], S->uhi[i]);
+    }
+    for (int i = 0; i < N * ni; i++)
+        DZ(S->dvL[i], S->dvU[i], S->vL[i], S->vU[i], S->s[i], S->ds[i], S->clo[i], S->chi[i]);
+#undef DZ
+}
+
 /* Newton direction with the stored factorisation for constraint residuals (rdyn, rin, req): the
  * primal-dual step (dx, du, dlam, dye), the slack-row steps (dyi, ds) and the bound-multiplier steps. */
 static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *rin, const double *req) {
@@ -675,39 +723,244 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
             memcpy(ynext, y, sizeof(double) * mb);
         }
     }
-    for (int k = 0; k < N; k++) {
-        const double *Ji = S->Ji + (size_t)k * ni * nv;
+    slack_and_bound_steps(S, mu, rin);
+}
+
+
+/* ---- Riccati factorisation and direction (mfg_opts.riccati; the device's csrc/gipm.hip recursion) ----
+ * Stage k eliminates u_k and the equality rows attached to it -- the state rows of node k+1 through the
+ * dynamics (J_e,k+1 [A_k | B_k]) and the mixed rows of stage k (J_m,k) -- with the stage block
+ *   K_k = [[Q_uu, D_u^T], [D_u, -dc]],  Q_uu = H_uu + B^T P_{k+1} B,
+ * and carries the value function P_k = Q_xx + R^T K_k^{-1}... (R = [Q_ux; D_x]).  The KKT matrix has the
+ * inertia (n_primal, n_dual, 0) iff every K_k has inertia (nu, rows) (Sylvester). */
+static int kkt_factor_ric(ws_t *S, double dw, double dc, double d1) {
+    const mfg_ocp *P = S->P;
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne, nes = S->nes, nk = S->nk;
+    S->dw = dw; S->dc = dc; S->d1 = d1;
+    double Pn[GX * GX], H[GV * GV], T1[GX * GU], T2[GX * GX], K[BKMAX * BKMAX], Rh[BKMAX * GX], Qxx[GX * GX];
+    double Dd[GI];
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < nx; j++) Pn[i * nx + j] = (i == j) ? S->Sx[N * nx + i] + dw : 0.0;
+    for (int k = N - 1; k >= 0; k--) {
+        const double *A = S->Af + (size_t)k * nx * nx, *B = S->Bf + (size_t)k * nx * nu;
+        const double *W = S->W + (size_t)k * nv * nv, *Ji = S->Ji + (size_t)k * ni * nv;
+        const double *Je = S->Je + (size_t)k * ne * nv, *Jn = S->Je + (size_t)(k + 1) * ne * nv;
+        const int en = (k + 1 < N) && EQ_ON(S, k + 1, 0) && nes > 0;
+        memcpy(S->Pg + (size_t)k * nx * nx, Pn, sizeof(double) * nx * nx);
         for (int q = 0; q < ni; q++) {
-            const int i = k * ni + q;
-            if (!CACT(S, k, q)) { S->dyi[i] = 0; S->ds[i] = 0; continue; }
-            double jd = 0;
-            for (int a = 0; a < nx; a++) jd += Ji[q * nv + a] * S->dx[k * nx + a];
-            for (int a = 0; a < nu; a++) jd += Ji[q * nv + nx + a] * S->du[k * nu + a];
-            const double sg = S->Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
-            const double rs = S->gs[i] - S->yi[i];
-            S->dyi[i] = Dd * (jd + rin[i] + rs / sg);
-            S->ds[i] = (S->dyi[i] - rs) / sg;
+            const double sg = S->Ss[k * ni + q] + dw;
+            Dd[q] = CACT(S, k, q) ? sg / (1.0 + dc * sg) : 0.0;
         }
-    }
-#define DZ(dzl, dzu, zl, zu, v, dv, lo, hi)                                              \
-    do {                                                                                 \
-        dzl = dzu = 0;                                                                   \
-        if (hasb(lo)) dzl = mu / ((v) - (lo)) - (zl) - (zl) / ((v) - (lo)) * (dv);       \
-        if (hasb(hi)) dzu = mu / ((hi) - (v)) - (zu) + (zu) / ((hi) - (v)) * (dv);       \
-    } while (0)
-    for (int k = 0; k <= N; k++)
+        for (int a = 0; a < nv; a++)
+            for (int c = 0; c < nv; c++) {
+                double v;
+                if (!vfree(S, k, a) || !vfree(S, k, c)) {
+                    v = (a == c) ? 1.0 : 0.0;
+                } else {
+                    v = W[a * nv + c];
+                    for (int q = 0; q < ni; q++) v += Ji[q * nv + a] * Dd[q] * Ji[q * nv + c];
+                    if (a == c) {
+                        v += dw;
+                        if (a < nx) v += S->Sx[k * nx + a];
+                        else {
+                            v += S->Su[k * nu + a - nx];
+                            if (a - nx >= P->tier1_from && a - nx < P->tier1_to) v += d1;
+                        }
+                    }
+                }
+                H[a * nv + c] = v;
+            }
+        for (int i = 0; i < nx; i++) {
+            for (int c = 0; c < nu; c++) {
+                double acc = 0.0;
+                for (int l = 0; l < nx; l++) acc += Pn[i * nx + l] * B[l * nu + c];
+                T1[i * nu + c] = acc;
+            }
+            for (int j = 0; j < nx; j++) {
+                double acc = 0.0;
+                for (int l = 0; l < nx; l++) acc += Pn[i * nx + l] * A[l * nx + j];
+                T2[i * nx + j] = acc;
+            }
+        }
+        for (int a = 0; a < nk; a++)
+            for (int c = 0; c < nk; c++) {
+                double v = 0.0;
+                if (a < nu && c < nu) {
+                    if (S->ufix[k * nu + a] || S->ufix[k * nu + c]) v = (a == c) ? 1.0 : 0.0;
+                    else {
+                        v = H[(nx + a) * nv + nx + c];
+                        for (int l = 0; l < nx; l++) v += B[l * nu + a] * T1[l * nu + c];
+                    }
+                } else if (a >= nu && c >= nu) {
+                    const int ee = a - nu;
+                    v = (a == c) ? ((ee >= nes || en) ? -dc : -1.0) : 0.0;
+                } else {
+                    const int ee = (a >= nu ? a : c) - nu, uu = a >= nu ? c : a;
+                    if (S->ufix[k * nu + uu]) v = 0.0;
+                    else if (ee >= nes) v = Je[ee * nv + nx + uu];  /* mixed row of stage k */
+                    else if (en)
+                        for (int l = 0; l < nx; l++) v += Jn[ee * nv + l] * B[l * nu + uu];
+                }
+                K[a * nk + c] = v;
+            }
+        for (int a = 0; a < nk; a++)
+            for (int j = 0; j < nx; j++) {
+                double v = 0.0;
+                if (k > 0) {
+                    if (a < nu) {
+                        if (!S->ufix[k * nu + a]) {
+                            v = H[(nx + a) * nv + j];
+                            for (int l = 0; l < nx; l++) v += B[l * nu + a] * T2[l * nx + j];
+                        }
+                    } else if (a - nu >= nes) {
+                        v = Je[(a - nu) * nv + j];
+                    } else if (en) {
+                        for (int l = 0; l < nx; l++) v += Jn[(a - nu) * nv + l] * A[l * nx + j];
+                    }
+                }
+                Rh[a * nx + j] = v;
+            }
+        for (int i = 0; i < nx; i++)
+            for (int j = 0; j < nx; j++) {
+                double v = H[i * nv + j];
+                for (int l = 0; l < nx; l++) v += A[l * nx + i] * T2[l * nx + j];
+                Qxx[i * nx + j] = v;
+            }
+        double *Kk = S->Kst + (size_t)k * nk * nk;
+        int *pp = S->Kpp + (size_t)k * 2 * nk;
+        memcpy(Kk, K, sizeof(double) * nk * nk);
+        int np, nn, nz;
+        bk_factor(Kk, nk, pp, pp + nk, &np, &nn, &nz);
+        if (nz) return 2;
+        if (np != nu || nn != ne) return 1;
+        double *Fk = S->Fg + (size_t)k * nk * nx;
         for (int j = 0; j < nx; j++) {
-            const int i = k * nx + j;
-            if (k == 0) { S->dzxL[i] = S->dzxU[i] = 0; continue; }
-            DZ(S->dzxL[i], S->dzxU[i], S->zxL[i], S->zxU[i], S->x[i], S->dx[i], S->xlo[j], S->xhi[j]);
+            double col[BKMAX];
+            for (int a = 0; a < nk; a++) col[a] = -Rh[a * nx + j];
+            bk_solve(Kk, nk, pp, pp + nk, col);
+            for (int a = 0; a < nk; a++) Fk[a * nx + j] = col[a];
         }
-    for (int i = 0; i < N * nu; i++) {
-        if (S->ufix[i]) { S->dzuL[i] = S->dzuU[i] = 0; continue; }
-        DZ(S->dzuL[i], S->dzuU[i], S->zuL[i], S->zuU[i], S->u[i], S->du[i], S->ulo[i], S->uhi[i]);
+        if (k > 0) {
+            double Pt[GX * GX];
+            for (int i = 0; i < nx; i++)
+                for (int j = 0; j < nx; j++) {
+                    double acc = Qxx[i * nx + j];
+                    for (int a = 0; a < nk; a++) acc += Rh[a * nx + i] * Fk[a * nx + j];
+                    Pt[i * nx + j] = acc;
+                }
+            for (int i = 0; i < nx; i++)
+                for (int j = 0; j < nx; j++) Pn[i * nx + j] = 0.5 * (Pt[i * nx + j] + Pt[j * nx + i]);
+        }
     }
-    for (int i = 0; i < N * ni; i++)
-        DZ(S->dvL[i], S->dvU[i], S->vL[i], S->vU[i], S->s[i], S->ds[i], S->clo[i], S->chi[i]);
-#undef DZ
+    return 0;
+}
+
+static void kkt_direction_ric(ws_t *S, double mu, const double *rdyn, const double *rin, const double *req) {
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne, nes = S->nes, nk = S->nk;
+    const double dw = S->dw, dc = S->dc;
+    double pvs[GX], vx[GV], tv[GX], zv[BKMAX], dxs[GX], dxn[GX], duv[BKMAX];
+    for (int j = 0; j < nx; j++) pvs[j] = S->gx[N * nx + j] - S->lam[(N - 1) * nx + j];
+    for (int k = N - 1; k >= 0; k--) {
+        const double *A = S->Af + (size_t)k * nx * nx, *B = S->Bf + (size_t)k * nx * nu;
+        const double *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + (size_t)k * ne * nv;
+        const double *Jn = S->Je + (size_t)(k + 1) * ne * nv, *Pk = S->Pg + (size_t)k * nx * nx;
+        const int en = (k + 1 < N) && EQ_ON(S, k + 1, 0) && nes > 0;
+        memcpy(S->pvg + (size_t)k * nx, pvs, sizeof(double) * nx);
+        for (int a = 0; a < nv; a++) {
+            double g = 0.0;
+            if (vfree(S, k, a)) {
+                g = S->gl[k * nv + a];
+                for (int q = 0; q < ni; q++) {
+                    const int i = k * ni + q;
+                    double w = S->yi[i];
+                    if (CACT(S, k, q)) {
+                        const double sg = S->Ss[i] + dw, D = sg / (1.0 + dc * sg);
+                        w += D * (rin[i] + (S->gs[i] - S->yi[i]) / sg);
+                    }
+                    g += Ji[q * nv + a] * w;
+                }
+                if (a < nx) {
+                    g += S->gx[k * nx + a] - (k > 0 ? S->lam[(k - 1) * nx + a] : 0.0);
+                    for (int jj = 0; jj < nx; jj++) g += A[jj * nx + a] * S->lam[k * nx + jj];
+                } else {
+                    g += S->gu[k * nu + a - nx];
+                    for (int jj = 0; jj < nx; jj++) g += B[jj * nu + a - nx] * S->lam[k * nx + jj];
+                }
+                for (int e = 0; e < ne; e++)
+                    if (EQ_ON(S, k, e) && (e >= nes || a < nx)) g += Je[e * nv + a] * S->ye[k * ne + e];
+            }
+            vx[a] = g;
+        }
+        for (int j = 0; j < nx; j++) {
+            double acc = pvs[j];
+            for (int l = 0; l < nx; l++) acc += Pk[j * nx + l] * rdyn[k * nx + l];
+            tv[j] = acc;
+        }
+        for (int a = 0; a < nk; a++) {
+            double z = 0.0;
+            if (a < nu) {
+                if (!S->ufix[k * nu + a]) {
+                    z = vx[nx + a];
+                    for (int l = 0; l < nx; l++) z += B[l * nu + a] * tv[l];
+                }
+            } else if (a - nu >= nes) {
+                z = req[k * ne + a - nu];
+            } else if (en) {
+                const int ee = a - nu;
+                z = req[(k + 1) * ne + ee];
+                for (int l = 0; l < nx; l++) z += Jn[ee * nv + l] * rdyn[k * nx + l];
+            }
+            zv[a] = z;
+        }
+        const double *Kk = S->Kst + (size_t)k * nk * nk, *Fk = S->Fg + (size_t)k * nk * nx;
+        const int *pp = S->Kpp + (size_t)k * 2 * nk;
+        for (int a = 0; a < nk; a++) duv[a] = -zv[a];
+        bk_solve(Kk, nk, pp, pp + nk, duv);
+        memcpy(S->kvg + (size_t)k * nk, duv, sizeof(double) * nk);
+        if (k > 0) {
+            for (int j = 0; j < nx; j++) {
+                double acc = vx[j];
+                for (int l = 0; l < nx; l++) acc += A[l * nx + j] * tv[l];
+                for (int a = 0; a < nk; a++) acc += Fk[a * nx + j] * zv[a];
+                dxn[j] = acc;
+            }
+            memcpy(pvs, dxn, sizeof(double) * nx);
+        }
+    }
+    for (int j = 0; j < nx; j++) { dxs[j] = 0.0; S->dx[j] = 0.0; }
+    for (int e = 0; e < ne; e++) S->dye[e] = 0.0;
+    for (int k = 0; k < N; k++) {
+        const double *A = S->Af + (size_t)k * nx * nx, *B = S->Bf + (size_t)k * nx * nu;
+        const double *Jn = S->Je + (size_t)(k + 1) * ne * nv, *Pk = S->Pg + (size_t)k * nx * nx;
+        const double *Fk = S->Fg + (size_t)k * nk * nx, *kv = S->kvg + (size_t)k * nk;
+        const int en = (k + 1 < N) && EQ_ON(S, k + 1, 0) && nes > 0;
+        for (int a = 0; a < nk; a++) {
+            double acc = kv[a];
+            for (int j = 0; j < nx; j++) acc += Fk[a * nx + j] * dxs[j];
+            if (a < nu && S->ufix[k * nu + a]) acc = 0.0;
+            duv[a] = acc;
+            if (a < nu) S->du[k * nu + a] = acc;
+        }
+        for (int j = 0; j < nx; j++) {
+            double acc = rdyn[k * nx + j];
+            for (int l = 0; l < nx; l++) acc += A[j * nx + l] * dxs[l];
+            for (int c = 0; c < nu; c++) acc += B[j * nu + c] * duv[c];
+            dxn[j] = acc;
+        }
+        for (int j = 0; j < nx; j++) {
+            double acc = S->pvg[(size_t)k * nx + j];
+            for (int l = 0; l < nx; l++) acc += Pk[j * nx + l] * dxn[l];
+            if (en)
+                for (int ee = 0; ee < nes; ee++) acc += Jn[ee * nv + j] * duv[nu + ee];
+            S->dlam[k * nx + j] = acc;
+            S->dx[(k + 1) * nx + j] = dxn[j];
+        }
+        if (k + 1 < N)
+            for (int ee = 0; ee < nes; ee++) S->dye[(k + 1) * ne + ee] = en ? duv[nu + ee] : 0.0;
+        for (int m = nes; m < ne; m++) S->dye[k * ne + m] = duv[nu + m];
+        memcpy(dxs, dxn, sizeof(double) * nx);
+    }
+    slack_and_bound_steps(S, mu, rin);
 }
 
 /* fraction to the boundary of the current direction */
@@ -896,6 +1149,14 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     S->trdyn = dal((size_t)N * nx); S->trin = dal(NI); S->treq = dal(NE);
     S->sdyn = dal((size_t)N * nx); S->sin_ = dal(NI); S->seq = dal(NE);
     S->bk = dal(3 * NX1 + 3 * NU + 4 * NI + (size_t)N * nx + NE);
+    S->ric = O->riccati;
+    S->nk = nu + ne;
+    if (S->ric) {
+        if (S->nk > BKMAX) return -2;
+        S->Pg = dal((size_t)N * nx * nx); S->Kst = dal((size_t)N * S->nk * S->nk); S->Fg = dal((size_t)N * S->nk * nx);
+        S->pvg = dal((size_t)N * nx); S->kvg = dal((size_t)N * S->nk);
+        S->Kpp = (int *)calloc((size_t)N * 2 * S->nk, sizeof(int));
+    }
     S->perm = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
     S->piv = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
 
@@ -1102,7 +1363,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
         if (tier == 1) d1 = reg; else if (tier == 2) dw = reg;
         for (tries = 0; tries < 60; tries++) {
             t_ph = wall_s();
-            const int fr = kkt_factor(S, dw, dc, d1);
+            const int fr = S->ric ? kkt_factor_ric(S, dw, dc, d1) : kkt_factor(S, dw, dc, d1);
             ts[1] += wall_s() - t_ph;
             if (fr == 0) { factor_ok = 1; break; }
             if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
@@ -1129,7 +1390,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
         /* ---- Newton direction for the residuals of the current point ---- */
         residuals_cached(S, S->rdyn, S->rin, S->req);
         t_ph = wall_s();
-        kkt_direction(S, mu, S->rdyn, S->rin, S->req);
+        (S->ric ? kkt_direction_ric : kkt_direction)(S, mu, S->rdyn, S->rin, S->req);
         ts[2] += wall_s() - t_ph;
         double ap, az;
         ftb(S, tau_fb, &ap, &az);
@@ -1168,7 +1429,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
                 for (int p = 0; p < O->max_soc; p++) {
                     save_direction(S);
                     t_ph = wall_s();
-                    kkt_direction(S, mu, S->sdyn, S->sin_, S->seq);
+                    (S->ric ? kkt_direction_ric : kkt_direction)(S, mu, S->sdyn, S->sin_, S->seq);
                     ts[2] += wall_s() - t_ph;
                     double aps, azs;
                     ftb(S, tau_fb, &aps, &azs);
@@ -1275,6 +1536,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
                      &S->trdyn, &S->trin, &S->treq, &S->sdyn, &S->sin_, &S->seq, &S->bk};
     for (size_t i = 0; i < sizeof pp / sizeof pp[0]; i++) free(*pp[i]);
     free(S->ufix); free(S->perm); free(S->piv);
+    if (S->ric) { free(S->Pg); free(S->Kst); free(S->Fg); free(S->pvg); free(S->kvg); free(S->Kpp); }
     return 0;
 }
 

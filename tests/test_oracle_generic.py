@@ -143,3 +143,32 @@ def test_thermal_c2_variant_solves():
     # without the thermal state the same force problem reaches the same optimum (bound inactive)
     w0, r0 = G.solve(PR.pilz6_bench(N=N), F_init=PR.BENCH_F_INIT, max_iter=300, max_soc=4)
     assert abs(r.obj - r0.obj) < 1e-4 * abs(r0.obj)
+
+
+@pytest.mark.parametrize("case", ["c1", "c2", "thermal", "centauro", "box"])
+def test_riccati_factorisation_matches_block_tridiagonal(golden, case):
+    """mfg_opts.riccati: the host IPM factors the KKT by the device's Riccati recursion (csrc/gipm.hip, stage
+    blocks with the Sylvester inertia test) instead of the checker's block-tridiagonal Bunch-Kaufman: the same
+    iterations and the same solution to round-off on every family (the CPU baseline's KKT algorithm)."""
+    if case == "c1":
+        spec, kw = PR.pilz3_working(N=30), {}
+    elif case == "c2":
+        spec, kw = PR.pilz6_bench(N=20), dict(F_init=PR.BENCH_F_INIT)
+    elif case == "thermal":
+        spec, kw = PR.pilz6_thermal(N=10, T0=79.0), dict(F_init=PR.BENCH_F_INIT)
+    elif case == "centauro":
+        spec = PR.centauro(N=6)
+        kw = dict(u_init=PR.centauro_u_init(spec))
+    else:
+        g, _ = golden["G1_box_N50"]
+        spec = dict(PR.box_dual(N=12, q0=g[:12]), pos_toll=1.0)
+        kw = dict(u_init=PR.box_u_init(spec))
+    w0, r0 = G.solve(spec, max_iter=500, max_soc=4, **kw)
+    w1, r1 = G.solve(spec, max_iter=500, max_soc=4, riccati=True, **kw)
+    assert r0.status == r1.status == 0 and r0.iter == r1.iter
+    if case == "box":  # the split of the forces along the box axis is weakly determined (DESIGN.md s.2)
+        N = spec["N"]
+        np.testing.assert_allclose(q_traj(w1, N), q_traj(w0, N), atol=1e-9)
+        np.testing.assert_allclose(w1, w0, atol=1e-4)
+    else:
+        np.testing.assert_allclose(w1, w0, atol=1e-9)

@@ -36,7 +36,7 @@ def _x_traj(w, nx, nu, N):
     return np.concatenate([w[:, None, :nx], w[:, nx:].reshape(w.shape[0], N, nu + nx)[:, :, nu:]], axis=1)
 
 
-def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0) -> dict:
+def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0, cases=("c3", "c4")) -> dict:
     import torch
 
     from mpc_fatigue_amd import problems as PR
@@ -46,6 +46,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
     stream = torch.cuda.current_stream(dev)
     rng = np.random.default_rng(seed)
     out = {}
+    todo = cases
     cases = []
     q0b = _golden_q0()
     sp3 = PR.box_shared_fatigue(N=100, q0=q0b)
@@ -56,6 +57,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
     q0c = np.asarray(sp4["q0"])
     X4 = np.hstack([q0c[None] + rng.uniform(-0.02, 0.02, (batch, 14)), np.tile(sp4["T0"], (batch, 1))])
     cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(u_init=PR.centauro_u_init(sp4), max_iter=500, max_soc=4)))
+    cases = [c for c in cases if c[0][:2] in todo]
     for name, spec, X, stages, kw in cases:
         gs = [GOCP(st) for st in stages]
         nx, nu, N = gs[0].nx, gs[0].nu, spec["N"]
@@ -66,19 +68,22 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
                  "kkt": torch.empty(batch, dtype=torch.float64, device=dev),
                  "obj": torch.empty(batch, dtype=torch.float64, device=dev)} for _ in stages]
 
-        def run():
+        def run(label, max_iter=None):
             prev = None
-            iters = []
-            for g, ob in zip(gs, bufs):
+            for i, (g, ob) in enumerate(zip(gs, bufs)):
                 ptr = {k: v.data_ptr() for k, v in ob.items()}
+                kw2 = dict(kw) if max_iter is None else dict(kw, max_iter=max_iter)
+                t = time.perf_counter()
                 g.solve_dev(x.data_ptr(), None, None if prev is None else prev.data_ptr(), None, batch, ptr,
-                            stream=stream.cuda_stream, **kw)
+                            stream=stream.cuda_stream, **kw2)
+                torch.cuda.synchronize(dev)
+                print(f"[generic_bench] {name} {label} stage {i}: {time.perf_counter() - t:.2f}s "
+                      f"converged {int((ob['status'] == 0).sum().item())}/{batch}", file=sys.stderr, flush=True)
                 prev = ob["w"]
-            torch.cuda.synchronize(dev)
 
-        run()  # warm-up (workspaces)
+        run("warm-up", max_iter=1)  # workspaces allocated, code loaded
         t0 = time.perf_counter()
-        run()
+        run("timed")
         dt = time.perf_counter() - t0
         st = bufs[-1]["status"].cpu().numpy()
         its = [int(b["iters"].sum().item()) for b in bufs]
@@ -117,8 +122,9 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--cases", default="c3,c4", help="comma list of c3 (shared budget N=100) and c4 (Centauro N=50)")
     ap.add_argument("--sample", type=int, default=2)
     a = ap.parse_args()
     import torch
     torch.cuda.init()
-    print(json.dumps(generic_extra(a.batch, a.sample)))
+    print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")))))
