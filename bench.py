@@ -178,24 +178,24 @@ def main() -> int:
     gathered = [None] * inflight  # event after the RCCL gather of each slot's last solutions
     torch.cuda.synchronize(dev)
 
-    def solve_on(i):
+    def solve_on(i, nb=hi - lo):
         torch.cuda.set_device(dev)  # the HIP device is per host thread
         o, st, ob, pt = slots[i]
         # N > 1: the new solve must not overwrite this slot's previous solutions before their gather has
         # read them; it waits for that gather alone, not for other slots' work
         if gathered[i] is not None:
             st.wait_event(gathered[i])
-        o.solve_dev(q0.data_ptr(), lref.data_ptr(), hi - lo, pt, stream=st.cuda_stream, **opts)
+        o.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=st.cuda_stream, **opts)
         st.synchronize()
 
-    def run_steps(K):
+    def run_steps(K, nb=hi - lo):
         from concurrent.futures import ThreadPoolExecutor
         with ThreadPoolExecutor(inflight) as ex:
             futs = []
             for s_ in range(K + inflight):
                 if s_ >= inflight:  # step s_ - inflight done: its slot is free (gather its solutions)
                     futs[s_ - inflight].result()
-                    if world > 1:
+                    if world > 1 and nb == hi - lo:
                         i = (s_ - inflight) % inflight
                         _, _, ob, _ = slots[i]
                         gather_solutions(ob["w"], ob["status"], rank, world)
@@ -203,7 +203,7 @@ def main() -> int:
                         ev.record(torch.cuda.current_stream(dev))  # the stream the gather ran on
                         gathered[i] = ev
                 if s_ < K:
-                    futs.append(ex.submit(solve_on, s_ % inflight))
+                    futs.append(ex.submit(solve_on, s_ % inflight, nb))
 
     run_steps(max(args.warmup, inflight))  # every slot warm (workspace allocated)
     torch.cuda.synchronize(dev)
@@ -321,8 +321,23 @@ def main() -> int:
             return float(np.median(ts)), int((o["status"] == 0).sum().item())
         if B >= 1024:
             t1024, c1024 = timed(1024, 3)
-            result["c5_shard_1024"] = {"value": c1024 / t1024, "unit": "horizons/s", "ms_per_step": t1024 * 1e3,
-                                       "converged": c1024, "note": "first 1024 horizons of the batch, median of 3"}
+            rec1024 = {"value": c1024 / t1024, "unit": "horizons/s", "ms_per_step": t1024 * 1e3,
+                       "converged": c1024, "note": "first 1024 horizons of the batch, one step alone, median of 3"}
+            if inflight > 1:
+                # the same shard at the bench's steps-in-flight setting (what each rank of the 8-GPU C5 run
+                # would do with --batch 1024): K consecutive 1024-horizon steps, `inflight` of them at a time
+                K = 4 * inflight
+                run_steps(inflight, 1024)
+                torch.cuda.synchronize(dev)
+                t = time.perf_counter()
+                run_steps(K, 1024)
+                torch.cuda.synchronize(dev)
+                dt = time.perf_counter() - t
+                cK = sum(int((sl[2]["status"][:1024] == 0).sum().item()) for sl in slots)
+                rec1024["inflight"] = {"value": cK / len(slots) * K / dt, "steps": K, "steps_in_flight": inflight,
+                                       "ms_per_step": dt / K * 1e3,
+                                       "note": f"{K} steps of the first 1024 horizons, {inflight} in flight"}
+            result["c5_shard_1024"] = rec1024
         t1, c1 = timed(1, 5)
         result["single_problem"] = {"ms_per_solve": t1 * 1e3, "converged": c1, "iters": int(out["iters"][0].item()),
                                     "note": "horizon 0 of the batch alone, median of 5 (host-polled every 4 iterations)"}
