@@ -532,4 +532,85 @@ __device__ void bk_solve_wave(const double *A, int m, const int *perm, const int
     __syncthreads();
 }
 
+
+// The same solve with one lane per right-hand-side column (nr <= 64): each lane runs the forward
+// substitution, the D solve and the back substitution of its own column in the order of
+// bk_solve_wave (so the results are identical), with no wave barrier between the pivot steps.
+// B and Y: row-major with leading dimension NR; lane c touches column c only.
+template <int LD, int NR>
+__device__ void bk_solve_cols_lane(const double *A, int m, const int *perm, const int *piv, double *B, int nr,
+                                   double *Y) {
+    const int c = lane_opaque();
+    if (c < nr) {
+        for (int i = 0; i < m; i++) Y[i * NR + c] = B[perm[i] * NR + c];
+        for (int k = 0; k < m;) {
+            const int s = piv[k] == 2 ? 2 : 1;
+            for (int i = k + s; i < m; i++) {
+                double y = Y[i * NR + c];
+                for (int t = 0; t < s; t++) y -= A[i * LD + k + t] * Y[(k + t) * NR + c];
+                Y[i * NR + c] = y;
+            }
+            k += s;
+        }
+        for (int i = 0; i < m; i++) {
+            if (piv[i] == 2) {
+                const double a = A[i * LD + i], bb = A[(i + 1) * LD + i], cc = A[(i + 1) * LD + i + 1];
+                const double det = a * cc - bb * bb;
+                const double y0 = Y[i * NR + c], y1 = Y[(i + 1) * NR + c];
+                Y[i * NR + c] = (cc * y0 - bb * y1) / det;
+                Y[(i + 1) * NR + c] = (a * y1 - bb * y0) / det;
+            } else if (piv[i] == 1) {
+                Y[i * NR + c] = Y[i * NR + c] / A[i * LD + i];
+            }
+        }
+        for (int k = m - 1; k >= 0;) {
+            const int k0 = (k > 0 && piv[k] == 0) ? k - 1 : k;
+            const int s = k - k0 + 1;
+            for (int t = 0; t < s; t++) {
+                double acc = Y[(k0 + t) * NR + c];
+                for (int i = k0 + s; i < m; i++) acc -= A[i * LD + k0 + t] * Y[i * NR + c];
+                Y[(k0 + t) * NR + c] = acc;
+            }
+            k = k0 - 1;
+        }
+        for (int i = 0; i < m; i++) B[perm[i] * NR + c] = Y[i * NR + c];
+    }
+    __syncthreads();
+}
+
+// C(i, j) = init(i, j) + sum_{l < KK} fa(l, i) fb(l, j) for i < M, j < NN from LDS operands: each lane
+// a TR x TC register tile, the operands of one l loaded once per tile.  Per entry the sum runs over l in
+// order from init, the arithmetic of the per-entry loop `v = init; for l: v += fa * fb` it replaces.
+template <int M, int NN, int KK, class Init, class FA, class FB, class Out>
+__device__ __forceinline__ void tile_gemm(int lane, Init init, FA fa, FB fb, Out out) {
+    constexpr int TR = (M + 7) / 8, TC = (NN + 7) / 8;
+    constexpr int BR = (M + TR - 1) / TR, BC = (NN + TC - 1) / TC;
+    static_assert(BR * BC <= 64, "tile grid larger than a wavefront");
+    if (lane < BR * BC) {
+        const int r0 = (lane / BC) * TR, c0 = (lane % BC) * TC;
+        double acc[TR][TC];
+#pragma unroll
+        for (int i = 0; i < TR; i++)
+#pragma unroll
+            for (int j = 0; j < TC; j++) acc[i][j] = init(min(r0 + i, M - 1), min(c0 + j, NN - 1));
+#pragma unroll 2
+        for (int l = 0; l < KK; l++) {
+            double av[TR], bv[TC];
+#pragma unroll
+            for (int i = 0; i < TR; i++) av[i] = fa(l, min(r0 + i, M - 1));
+#pragma unroll
+            for (int j = 0; j < TC; j++) bv[j] = fb(l, min(c0 + j, NN - 1));
+#pragma unroll
+            for (int i = 0; i < TR; i++)
+#pragma unroll
+                for (int j = 0; j < TC; j++) acc[i][j] += av[i] * bv[j];
+        }
+#pragma unroll
+        for (int i = 0; i < TR; i++)
+#pragma unroll
+            for (int j = 0; j < TC; j++)
+                if (r0 + i < M && c0 + j < NN) out(r0 + i, c0 + j, acc[i][j]);
+    }
+}
+
 }  // namespace mf

@@ -32,6 +32,7 @@ namespace mf {
 
 struct GState {
     double mu, nu, reg_last, E0, cviol, obj;
+    double dw_c, dc_c;  // the regularisation the accepted factorisation was made with (k_gkkt -> k_gls)
     int reg_tier, status, iter, n_ls_fail, n_ic, consec_fail, n_soc, pad;
 };
 enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INERTIA = 3 };
@@ -92,6 +93,32 @@ __device__ __forceinline__ void gsync() {
     __threadfence_block();
     __syncthreads();
 }
+
+// Diagnostic build only (-DMF_GSTAMPS, libmpcfatigue_gstamps.so): per-phase cycle counts of k_giter
+// accumulated in registers by every lane and added to a debug buffer by lane 0 once per launch
+#ifdef MF_GSTAMPS
+__device__ unsigned long long mf_gstamp_buf[32 * 1024];
+#define GSTAMP(slot)                                                                  \
+    do {                                                                              \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime();                         \
+        gst_acc_[slot] += t_ - gst_prev_;                                             \
+        gst_prev_ = t_;                                                               \
+    } while (0)
+#define GSTAMP_INIT                                                                   \
+    unsigned long long gst_acc_[32] = {0};                                            \
+    unsigned long long gst_prev_ = __builtin_amdgcn_s_memtime()
+#define GSTAMP_COUNT(slot, v) do { gst_acc_[slot] += (v); } while (0)
+#define GSTAMP_FLUSH                                                                  \
+    do {                                                                              \
+        if (lane == 0 && b < 1024)                                                    \
+            for (int s_ = 0; s_ < 32; s_++) mf_gstamp_buf[b * 32 + s_] += gst_acc_[s_]; \
+    } while (0)
+#else
+#define GSTAMP(slot) do {} while (0)
+#define GSTAMP_INIT do {} while (0)
+#define GSTAMP_COUNT(slot, v) do {} while (0)
+#define GSTAMP_FLUSH do {} while (0)
+#endif
 
 // first NJ joints of a DevModel in LDS
 template <int NJ> struct GModelLds {
@@ -244,15 +271,21 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         GState st;
         st.mu = P.mu_init; st.nu = 0.0; st.reg_last = 0.0; st.E0 = INFINITY; st.cviol = INFINITY; st.obj = 0.0;
         st.reg_tier = 0; st.status = GS_RUNNING; st.iter = 0; st.n_ls_fail = 0; st.n_ic = 0; st.consec_fail = 0;
-        st.n_soc = 0; st.pad = 0;
+        st.n_soc = 0; st.pad = 0; st.dw_c = 0.0; st.dc_c = 0.0;
         A.st[b] = st;
     }
 }
 
 // ============================================================== one interior-point iteration
-template <class FAM>
-__global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
-                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
+// Three launches per iteration, one wavefront per horizon each (giter_phase<FAM, PH>):
+//   PH 0 k_gpre  optimality error, convergence test, barrier update, Sigma / barrier gradients, residuals
+//   PH 1 k_gkkt  inertia-corrected Riccati factorisation and the Newton direction
+//   PH 2 k_gls   fraction to the boundary, l1-merit line search with second-order corrections, update
+// The phases share this one body (same arithmetic as a single kernel); each launch keeps only its own
+// phase's code and LDS, so register allocation and occupancy are per phase.
+template <class FAM, int PH>
+__device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                            const DevFrame *F1, const GParams &P, const GArrays &A, int batch) {
     using D = typename FAM::D;
     constexpr int NX = D::NX, NU = D::NU, NV = D::NV, NI = D::NI, NE = D::NE, NIA = D::NIA, NEA = D::NEA;
     constexpr int NM = D::NM, NET = D::NET;  // mixed rows c_m(x_k, u_k): multipliers at ye[k NET + NEA + m]
@@ -261,13 +294,32 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     if (b >= batch) return;
     GState st = A.st[b];
     if (st.status != GS_RUNNING) return;
-    GMODELS(FAM);
+    __shared__ GModels<FAM> Gm;
+    if constexpr (PH == 2) {
+        Gm.load(M0, M1, F0, F1);
+        __syncthreads();
+    }
+    const MArr M{&Gm.m[0].get(), &Gm.m[FAM::NM - 1].get()};
+    const FArr F{&Gm.f[0], &Gm.f[FAM::NM - 1]};
+    GSTAMP_INIT;
     __shared__ double Hs[NV * NV], Ps[NX * NX], T1[NX * NU], T2[NX * NX], Ab[NX * NX], Bb[NX * NU], Qxx[NX * NX];
     constexpr int KSTG = NK * LDK + 2 * NK;  // per stage: factored block, perm, piv
     constexpr int NYS = NK * (NX > 1 ? NX : 1);
     __shared__ double Ks[NK * LDK], Ys[NYS], Rh[NK * NX], Kf[NK * NX], Jn[NEA * NX], Dds[NIA];
     __shared__ int perm[NK], piv[NK];
     __shared__ double vx[NV], tv[NX], zv[NK], pvs[NX], dxs[NX], dxn[NX], duv[NK];
+    // stage k's record parts staged into LDS by coalesced lane-strided loads (stage_in): the inner
+    // loops of the stage then read LDS, not global memory; fixed-control / active-row flags alike
+    constexpr int NIA2 = NI > 0 ? NI : 1, NMA = NM > 0 ? NM : 1;
+    __shared__ double JIs[NIA2 * NV], JMs[NMA * NV];
+    __shared__ int fixs[NU], acts[NIA2];
+    // stage vectors (stage_vec): barrier Sigma of the stage's x / u / slack rows (factor), and for the
+    // direction's backward pass grad L_k, the barrier gradients, lambda_k, lambda_{k-1}, y_e,k, the slack
+    // weights w_q, rd_k, re_k, re_{k+1} and J_E of node k
+    constexpr int V_SX = 0, V_SU = V_SX + NX, V_SS = V_SU + NU, V_GL = V_SS + NIA2, V_GX = V_GL + NV,
+                  V_LK = V_GX + NX, V_LP = V_LK + NX, V_YE = V_LP + NX, V_GU = V_YE + NET, V_W = V_GU + NU,
+                  V_RD = V_W + NIA2, V_RE = V_RD + NX, V_RN = V_RE + NET, V_JE = V_RN + NEA, V_END = V_JE + NEA * NX;
+    __shared__ double Vs[V_END];
 
     const int N = P.N;
     const GSz<D> Z(N);
@@ -300,6 +352,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     double mu = st.mu, nu = st.nu;
 
     auto finish = [&](int status) {
+        GSTAMP_FLUSH;
         double f = 0.0;
         for (int k = lane; k < N; k += 64) f += R(k)[D::O_L];
         f = wave_sum(f);
@@ -313,6 +366,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         }
     };
 
+    if constexpr (PH == 0) {
     // ---------------- optimality error (IPOPT E_0, s_max scaling)
     double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sm = 0, sbm = 0;
     int nm = 0, nbm = 0;
@@ -417,7 +471,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         cinfm = wave_max(cm);
         Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
     }
-    const double tau_fb = fmax(tau_min, 1.0 - mu);
+    GSTAMP(0);
 
     // ---------------- barrier Sigma / gradients, residuals of the current point
     for (int e = lane; e < (N + 1) * NX; e += 64) {
@@ -454,105 +508,122 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         req[e] = ee < NEA ? ((ee < NE && eqon(k)) ? R(k)[D::O_CE + ee] : 0.0) : R(k)[D::O_CM + ee - NEA];
     }
     gsync();
+    GSTAMP(1);
+    GSTAMP_FLUSH;
+    if (lane == 0) {
+        st.mu = mu;
+        A.st[b] = st;
+    }
+    return;
+    }  // PH 0
+    const double tau_fb = fmax(tau_min, 1.0 - mu);
 
     // ---------------- Riccati factorisation with inertia test (stage blocks [[Quu, Du^T], [Du, -dc]])
     double dw_c = 0.0, dc_c = 0.0;
+    // stage k's A, B, J_I, J_M (and W into Hs), J_E of node k+1, the fixed-control and active-row flags
+    auto stage_in = [&](int k, bool withW) {
+        const double *rk = R(k);
+        const bool en = eqon(k + 1);
+        for (int e = lane; e < NX * NX; e += 64) Ab[e] = rk[D::O_A + e];
+        for (int e = lane; e < NX * NU; e += 64) Bb[e] = rk[D::O_B + e];
+        for (int e = lane; e < NI * NV; e += 64) JIs[e] = rk[D::O_JI + e];
+        for (int e = lane; e < NM * NV; e += 64) JMs[e] = rk[D::O_JM + e];
+        if (withW)
+            for (int e = lane; e < NV * NV; e += 64) Hs[e] = rk[D::O_W + e];
+        for (int e = lane; e < NEA * NX; e += 64) Jn[e] = (en && e < NE * NX) ? R(k + 1)[D::O_JE + e] : 0.0;
+        for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
+        for (int q = lane; q < NI; q += 64) acts[q] = cact(k, q) ? 1 : 0;
+    };
     auto factor = [&](double dw, double dc, double d1) -> int {
         for (int e = lane; e < NX * NX; e += 64) Ps[e] = (e / NX == e % NX) ? Sx[N * NX + e / NX] + dw : 0.0;
         __syncthreads();
         for (int k = N - 1; k >= 0; k--) {
-            const double *rk = R(k);
+            GSTAMP(2);
             const bool en = eqon(k + 1);
-            for (int e = lane; e < NX * NX; e += 64) {
-                Pg[(size_t)k * NX * NX + e] = Ps[e];
-                Ab[e] = rk[D::O_A + e];
-            }
-            for (int e = lane; e < NX * NU; e += 64) Bb[e] = rk[D::O_B + e];
-            for (int e = lane; e < NEA * NX; e += 64) Jn[e] = (en && e < NE * NX) ? R(k + 1)[D::O_JE + e] : 0.0;
+            for (int e = lane; e < NX * NX; e += 64) Pg[(size_t)k * NX * NX + e] = Ps[e];
+            stage_in(k, true);
+            for (int j = lane; j < NX; j += 64) Vs[V_SX + j] = Sx[k * NX + j];
+            for (int c = lane; c < NU; c += 64) Vs[V_SU + c] = Su[k * NU + c];
+            for (int q = lane; q < NI; q += 64) Vs[V_SS + q] = Ss[k * NIA + q];
+            gsync();
             for (int q = lane; q < NI; q += 64) {
-                const double sg = Ss[k * NIA + q] + dw;
-                Dds[q] = cact(k, q) ? sg / (1.0 + dc * sg) : 0.0;
+                const double sg = Vs[V_SS + q] + dw;
+                Dds[q] = acts[q] ? sg / (1.0 + dc * sg) : 0.0;
             }
             gsync();
-            for (int e = lane; e < NV * NV; e += 64) {
-                const int a = e / NV, c = e % NV;
-                const bool fa = a < NX ? (k == 0) : ufix(k * NU + a - NX);
-                const bool fc = c < NX ? (k == 0) : ufix(k * NU + c - NX);
-                double v;
-                if (fa || fc) {
-                    v = (a == c) ? 1.0 : 0.0;
-                } else {
-                    v = rk[D::O_W + e];
-                    for (int q = 0; q < NI; q++) v += rk[D::O_JI + q * NV + a] * Dds[q] * rk[D::O_JI + q * NV + c];
-                    if (a == c) {
+            GSTAMP(8);
+            // H = W + J_I^T D J_I (+ diagonal terms), in place over W (each lane its own tile)
+            tile_gemm<NV, NV, (NI > 0 ? NI : 1)>(
+                lane, [&](int a, int c) { return Hs[a * NV + c]; },
+                [&](int q, int a) { return NI > 0 ? JIs[q * NV + a] * Dds[q] : 0.0; },
+                [&](int q, int c) { return NI > 0 ? JIs[q * NV + c] : 0.0; },
+                [&](int a, int c, double v) {
+                    const bool fa = a < NX ? (k == 0) : fixs[a - NX];
+                    const bool fc = c < NX ? (k == 0) : fixs[c - NX];
+                    if (fa || fc) {
+                        v = (a == c) ? 1.0 : 0.0;
+                    } else if (a == c) {
                         v += dw;
-                        if (a < NX) v += Sx[k * NX + a];
+                        if (a < NX) v += Vs[V_SX + a];
                         else {
-                            v += Su[k * NU + a - NX];
+                            v += Vs[V_SU + a - NX];
                             if (a - NX >= P.tier1_from && a - NX < P.tier1_to) v += d1;
                         }
                     }
-                }
-                Hs[e] = v;
-            }
-            for (int e = lane; e < NX * NU; e += 64) {
-                const int i = e / NU, c = e % NU;
-                double acc = 0.0;
-                for (int l = 0; l < NX; l++) acc += Ps[i * NX + l] * Bb[l * NU + c];
-                T1[e] = acc;
-            }
-            for (int e = lane; e < NX * NX; e += 64) {
-                const int i = e / NX, j = e % NX;
-                double acc = 0.0;
-                for (int l = 0; l < NX; l++) acc += Ps[i * NX + l] * Ab[l * NX + j];
-                T2[e] = acc;
-            }
+                    Hs[a * NV + c] = v;
+                });
+            GSTAMP(9);
+            tile_gemm<NX, NU, NX>(
+                lane, [](int, int) { return 0.0; }, [&](int l, int i) { return Ps[i * NX + l]; },
+                [&](int l, int c) { return Bb[l * NU + c]; }, [&](int i, int c, double v) { T1[i * NU + c] = v; });
+            tile_gemm<NX, NX, NX>(
+                lane, [](int, int) { return 0.0; }, [&](int l, int i) { return Ps[i * NX + l]; },
+                [&](int l, int j) { return Ab[l * NX + j]; }, [&](int i, int j, double v) { T2[i * NX + j] = v; });
             __syncthreads();
+            GSTAMP(10);
+            tile_gemm<NU, NU, NX>(
+                lane, [&](int a, int c) { return Hs[(NX + a) * NV + NX + c]; },
+                [&](int l, int a) { return Bb[l * NU + a]; }, [&](int l, int c) { return T1[l * NU + c]; },
+                [&](int a, int c, double v) { Ks[a * LDK + c] = (fixs[a] || fixs[c]) ? ((a == c) ? 1.0 : 0.0) : v; });
             for (int e = lane; e < NK * NK; e += 64) {
                 const int a = e / NK, c = e % NK;
                 double v = 0.0;
                 if (a < NU && c < NU) {
-                    if (ufix(k * NU + a) || ufix(k * NU + c)) v = (a == c) ? 1.0 : 0.0;
-                    else {
-                        v = Hs[(NX + a) * NV + NX + c];
-                        for (int l = 0; l < NX; l++) v += Bb[l * NU + a] * T1[l * NU + c];
-                    }
+                    continue;  // the control block: tile_gemm above
                 } else if (a >= NU && c >= NU) {
                     v = (a == c) ? ((a - NU >= NEA || (en && a - NU < NE)) ? -dc : -1.0) : 0.0;
                 } else {
                     const int ee = (a >= NU ? a : c) - NU, uu = a >= NU ? c : a;
-                    if (ufix(k * NU + uu)) v = 0.0;
-                    else if (ee >= NEA) v = rk[D::O_JM + (ee - NEA) * NV + NX + uu];  // mixed row of stage k
+                    if (fixs[uu]) v = 0.0;
+                    else if (ee >= NEA) v = JMs[(ee - NEA) * NV + NX + uu];  // mixed row of stage k
                     else if (en && ee < NE)
                         for (int l = 0; l < NX; l++) v += Jn[ee * NX + l] * Bb[l * NU + uu];
                 }
                 Ks[a * LDK + c] = v;
             }
-            for (int e = lane; e < NK * NX; e += 64) {
+            tile_gemm<NU, NX, NX>(
+                lane, [&](int a, int j) { return Hs[(NX + a) * NV + j]; },
+                [&](int l, int a) { return Bb[l * NU + a]; }, [&](int l, int j) { return T2[l * NX + j]; },
+                [&](int a, int j, double v) { Rh[a * NX + j] = (k > 0 && !fixs[a]) ? v : 0.0; });
+            for (int e = NU * NX + lane; e < NK * NX; e += 64) {
                 const int a = e / NX, j = e % NX;
                 double v = 0.0;
                 if (k > 0) {
-                    if (a < NU) {
-                        if (!ufix(k * NU + a)) {
-                            v = Hs[(NX + a) * NV + j];
-                            for (int l = 0; l < NX; l++) v += Bb[l * NU + a] * T2[l * NX + j];
-                        }
-                    } else if (a - NU >= NEA) {
-                        v = rk[D::O_JM + (a - NU - NEA) * NV + j];
+                    if (a - NU >= NEA) {
+                        v = JMs[(a - NU - NEA) * NV + j];
                     } else if (en && a - NU < NE) {
                         for (int l = 0; l < NX; l++) v += Jn[(a - NU) * NX + l] * Ab[l * NX + j];
                     }
                 }
                 Rh[e] = v;
             }
-            for (int e = lane; e < NX * NX; e += 64) {
-                const int i = e / NX, j = e % NX;
-                double v = Hs[i * NV + j];
-                for (int l = 0; l < NX; l++) v += Ab[l * NX + i] * T2[l * NX + j];
-                Qxx[e] = v;
-            }
+            tile_gemm<NX, NX, NX>(
+                lane, [&](int i, int j) { return Hs[i * NV + j]; }, [&](int l, int i) { return Ab[l * NX + i]; },
+                [&](int l, int j) { return T2[l * NX + j]; }, [&](int i, int j, double v) { Qxx[i * NX + j] = v; });
             __syncthreads();
+            GSTAMP(11);
             const BKInertia in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+            GSTAMP(12);
             if (in.zero) return 2;
             if (in.pos != NU || in.neg != NET) return 1;
             // the stage factorisation is kept (the solves of the vector pass and of the second-order
@@ -562,20 +633,21 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             for (int e = lane; e < NK; e += 64) { kst[NK * LDK + e] = perm[e]; kst[NK * LDK + NK + e] = piv[e]; }
             for (int e = lane; e < NK * NX; e += 64) Kf[e] = -Rh[e];
             __syncthreads();
-            bk_solve_wave<LDK, NX>(Ks, NK, perm, piv, Kf, NX, Ys);
+            // one lane per right-hand side with the column in registers up to NK = 24 (register budget)
+            if constexpr (NK <= 24) bk_solve_cols<LDK, NX, NK>(Ks, perm, piv, Kf, NX);
+            else bk_solve_wave<LDK, NX>(Ks, NK, perm, piv, Kf, NX, Ys);
             for (int e = lane; e < NK * NX; e += 64) Fg[(size_t)k * NK * NX + e] = Kf[e];
             __syncthreads();
+            GSTAMP(13);
             if (k > 0) {
-                for (int e = lane; e < NX * NX; e += 64) {
-                    const int i = e / NX, j = e % NX;
-                    double acc = Qxx[e];
-                    for (int a = 0; a < NK; a++) acc += Rh[a * NX + i] * Kf[a * NX + j];
-                    T2[e] = acc;
-                }
+                tile_gemm<NX, NX, NK>(
+                    lane, [&](int i, int j) { return Qxx[i * NX + j]; }, [&](int a, int i) { return Rh[a * NX + i]; },
+                    [&](int a, int j) { return Kf[a * NX + j]; }, [&](int i, int j, double v) { T2[i * NX + j] = v; });
                 __syncthreads();
                 for (int e = lane; e < NX * NX; e += 64) Ps[e] = 0.5 * (T2[e] + T2[(e % NX) * NX + e / NX]);
                 __syncthreads();
             }
+            GSTAMP(14);
         }
         return 0;
     };
@@ -589,77 +661,96 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             const double *rk = R(k);
             const bool en = eqon(k + 1);
             for (int j = lane; j < NX; j += 64) pvg[k * NX + j] = pvs[j];
+            // every operand of the stage into LDS in one round trip: the record parts, P_{k+1} (T2),
+            // the stored stage factorisation (Ks, perm, piv) and feedback (Kf), the stage vectors
+            stage_in(k, false);
+            {
+                const double *kst = Kg + (size_t)k * KSTG;
+                for (int e = lane; e < NX * NX; e += 64) T2[e] = Pg[(size_t)k * NX * NX + e];
+                for (int e = lane; e < NK * LDK; e += 64) Ks[e] = kst[e];
+                for (int e = lane; e < NK; e += 64) {
+                    perm[e] = (int)kst[NK * LDK + e];
+                    piv[e] = (int)kst[NK * LDK + NK + e];
+                }
+                for (int e = lane; e < NK * NX; e += 64) Kf[e] = Fg[(size_t)k * NK * NX + e];
+            }
+            for (int a = lane; a < NV; a += 64) Vs[V_GL + a] = rk[D::O_GL + a];
+            for (int j = lane; j < NX; j += 64) {
+                Vs[V_GX + j] = gx[k * NX + j];
+                Vs[V_LK + j] = lam[k * NX + j];
+                Vs[V_LP + j] = k > 0 ? lam[(k - 1) * NX + j] : 0.0;
+                Vs[V_RD + j] = rd[k * NX + j];
+            }
+            for (int c = lane; c < NU; c += 64) Vs[V_GU + c] = gu[k * NU + c];
+            for (int ee = lane; ee < NET; ee += 64) {
+                Vs[V_YE + ee] = ye[k * NET + ee];
+                Vs[V_RE + ee] = re[k * NET + ee];
+            }
+            for (int ee = lane; ee < NEA; ee += 64) Vs[V_RN + ee] = (k + 1 < N) ? re[(k + 1) * NET + ee] : 0.0;
+            for (int e = lane; e < NEA * NX; e += 64) Vs[V_JE + e] = (eqon(k) && e < NE * NX) ? rk[D::O_JE + e] : 0.0;
+            // slack-row weights of the stage (vx: the J_I^T w term)
+            for (int q = lane; q < NI; q += 64) {
+                const int i = k * NIA + q;
+                double w = yi[i];
+                if (cact(k, q)) {
+                    const double sg = Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
+                    w += Dd * (ri[i] + (gs[i] - yi[i]) / sg);
+                }
+                Vs[V_W + q] = w;
+            }
+            gsync();
             for (int a = lane; a < NV; a += 64) {
-                const bool fa = a < NX ? (k == 0) : ufix(k * NU + a - NX);
+                const bool fa = a < NX ? (k == 0) : fixs[a - NX];
                 double g = 0.0;
                 if (!fa) {
-                    g = rk[D::O_GL + a];
-                    for (int q = 0; q < NI; q++) {
-                        const int i = k * NIA + q;
-                        double w = yi[i];
-                        if (cact(k, q)) {
-                            const double sg = Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
-                            w += Dd * (ri[i] + (gs[i] - yi[i]) / sg);
-                        }
-                        g += rk[D::O_JI + q * NV + a] * w;
-                    }
+                    g = Vs[V_GL + a];
+                    for (int q = 0; q < NI; q++) g += JIs[q * NV + a] * Vs[V_W + q];
                     if (a < NX) {
-                        g += gx[k * NX + a] - (k > 0 ? lam[(k - 1) * NX + a] : 0.0);
-                        for (int jj = 0; jj < NX; jj++) g += rk[D::O_A + jj * NX + a] * lam[k * NX + jj];
+                        g += Vs[V_GX + a] - Vs[V_LP + a];
+                        for (int jj = 0; jj < NX; jj++) g += Ab[jj * NX + a] * Vs[V_LK + jj];
                         if (eqon(k))
-                            for (int ee = 0; ee < NE; ee++) g += rk[D::O_JE + ee * NX + a] * ye[k * NET + ee];
+                            for (int ee = 0; ee < NE; ee++) g += Vs[V_JE + ee * NX + a] * Vs[V_YE + ee];
                     } else {
-                        g += gu[k * NU + a - NX];
-                        for (int jj = 0; jj < NX; jj++) g += rk[D::O_B + jj * NU + a - NX] * lam[k * NX + jj];
+                        g += Vs[V_GU + a - NX];
+                        for (int jj = 0; jj < NX; jj++) g += Bb[jj * NU + a - NX] * Vs[V_LK + jj];
                     }
-                    for (int m = 0; m < NM; m++) g += rk[D::O_JM + m * NV + a] * ye[k * NET + NEA + m];
+                    for (int m = 0; m < NM; m++) g += JMs[m * NV + a] * Vs[V_YE + NEA + m];
                 }
                 vx[a] = g;
             }
             for (int j = lane; j < NX; j += 64) {
                 double acc = pvs[j];
-                for (int l = 0; l < NX; l++) acc += Pg[(size_t)k * NX * NX + j * NX + l] * rd[k * NX + l];
+                for (int l = 0; l < NX; l++) acc += T2[j * NX + l] * Vs[V_RD + l];
                 tv[j] = acc;
             }
             gsync();
             for (int a = lane; a < NK; a += 64) {
                 double z = 0.0;
                 if (a < NU) {
-                    if (!ufix(k * NU + a)) {
+                    if (!fixs[a]) {
                         z = vx[NX + a];
-                        for (int l = 0; l < NX; l++) z += rk[D::O_B + l * NU + a] * tv[l];
+                        for (int l = 0; l < NX; l++) z += Bb[l * NU + a] * tv[l];
                     }
                 } else if (a - NU >= NEA) {
-                    z = re[k * NET + a - NU];  // mixed row of stage k
+                    z = Vs[V_RE + a - NU];  // mixed row of stage k
                 } else if (en && a - NU < NE) {
                     const int ee = a - NU;
-                    z = re[(k + 1) * NET + ee];
-                    for (int l = 0; l < NX; l++) z += R(k + 1)[D::O_JE + ee * NX + l] * rd[k * NX + l];
+                    z = Vs[V_RN + ee];
+                    for (int l = 0; l < NX; l++) z += Jn[ee * NX + l] * Vs[V_RD + l];
                 }
                 zv[a] = z;
+                duv[a] = -z;
             }
-            gsync();
-            {
-                const double *kst = Kg + (size_t)k * KSTG;
-                for (int e = lane; e < NK * LDK; e += 64) Ks[e] = kst[e];
-                for (int e = lane; e < NK; e += 64) {
-                    perm[e] = (int)kst[NK * LDK + e];
-                    piv[e] = (int)kst[NK * LDK + NK + e];
-                    duv[e] = -zv[e];
-                }
-                __syncthreads();
-                bk_solve_wave<LDK, 1>(Ks, NK, perm, piv, duv, 1, Ys);
-                for (int a = lane; a < NK; a += 64) kvg[k * NK + a] = duv[a];
-            }
+            wave_lds_sync();
+            bk_solve_wave<LDK, 1>(Ks, NK, perm, piv, duv, 1, Ys);
+            for (int a = lane; a < NK; a += 64) kvg[k * NK + a] = duv[a];
             if (k > 0)
                 for (int j = lane; j < NX; j += 64) {
                     double acc = vx[j];
-                    for (int l = 0; l < NX; l++) acc += rk[D::O_A + l * NX + j] * tv[l];
-                    for (int a = 0; a < NK; a++) acc += Fg[(size_t)k * NK * NX + a * NX + j] * zv[a];
-                    dxn[j] = acc;
+                    for (int l = 0; l < NX; l++) acc += Ab[l * NX + j] * tv[l];
+                    for (int a = 0; a < NK; a++) acc += Kf[a * NX + j] * zv[a];
+                    pvs[j] = acc;
                 }
-            gsync();
-            for (int j = lane; j < NX; j += 64) pvs[j] = dxn[j];
             gsync();
         }
         // forward sweep
@@ -669,26 +760,35 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         for (int k = 0; k < N; k++) {
             const double *rk = R(k);
             const bool en = eqon(k + 1);
+            // the stage's operands into LDS first (one round trip), then three LDS-only phases
+            for (int e = lane; e < NX * NX; e += 64) { Ab[e] = rk[D::O_A + e]; T2[e] = Pg[(size_t)k * NX * NX + e]; }
+            for (int e = lane; e < NX * NU; e += 64) Bb[e] = rk[D::O_B + e];
+            for (int e = lane; e < NK * NX; e += 64) Kf[e] = Fg[(size_t)k * NK * NX + e];
+            for (int e = lane; e < NEA * NX; e += 64) Jn[e] = (en && e < NE * NX) ? R(k + 1)[D::O_JE + e] : 0.0;
+            for (int a = lane; a < NK; a += 64) zv[a] = kvg[k * NK + a];
+            for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
+            for (int j = lane; j < NX; j += 64) { tv[j] = pvg[k * NX + j]; vx[j] = rd[k * NX + j]; }
+            gsync();
             for (int a = lane; a < NK; a += 64) {
-                double acc = kvg[k * NK + a];
-                for (int j = 0; j < NX; j++) acc += Fg[(size_t)k * NK * NX + a * NX + j] * dxs[j];
-                if (a < NU && ufix(k * NU + a)) acc = 0.0;
+                double acc = zv[a];
+                for (int j = 0; j < NX; j++) acc += Kf[a * NX + j] * dxs[j];
+                if (a < NU && fixs[a]) acc = 0.0;
                 duv[a] = acc;
                 if (a < NU) du[k * NU + a] = acc;
             }
             gsync();
             for (int j = lane; j < NX; j += 64) {
-                double acc = rd[k * NX + j];
-                for (int l = 0; l < NX; l++) acc += rk[D::O_A + j * NX + l] * dxs[l];
-                for (int c = 0; c < NU; c++) acc += rk[D::O_B + j * NU + c] * duv[c];
+                double acc = vx[j];
+                for (int l = 0; l < NX; l++) acc += Ab[j * NX + l] * dxs[l];
+                for (int c = 0; c < NU; c++) acc += Bb[j * NU + c] * duv[c];
                 dxn[j] = acc;
             }
             gsync();
             for (int j = lane; j < NX; j += 64) {
-                double acc = pvg[k * NX + j];
-                for (int l = 0; l < NX; l++) acc += Pg[(size_t)k * NX * NX + j * NX + l] * dxn[l];
+                double acc = tv[j];
+                for (int l = 0; l < NX; l++) acc += T2[j * NX + l] * dxn[l];
                 if (en)
-                    for (int ee = 0; ee < NE; ee++) acc += R(k + 1)[D::O_JE + ee * NX + j] * duv[NU + ee];
+                    for (int ee = 0; ee < NE; ee++) acc += Jn[ee * NX + j] * duv[NU + ee];
                 dlam[k * NX + j] = acc;
                 dx[(k + 1) * NX + j] = dxn[j];
             }
@@ -850,6 +950,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         gsync();
     };
 
+    if constexpr (PH == 1) {
     // ---------------- inertia correction
     double dw = 0.0, dc = P.dc_always ? 1e-8 * pow(mu, 0.25) : 0.0, d1 = 0.0;
     int tier = st.reg_tier, step_no = 0;
@@ -859,6 +960,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     const bool has_t1 = P.tier1_to > P.tier1_from;
     bool factor_ok = false;
     for (int tries = 0; tries < 60; tries++) {
+        GSTAMP_COUNT(20, 1);
         const int fr = factor(dw, dc, d1);
         if (fr == 0) { factor_ok = true; break; }
         if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
@@ -882,9 +984,21 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     st.reg_last = reg;
     dw_c = dw;
     dc_c = dc;
+    GSTAMP(2);
+    direction(rdyn, rin, req);
+    GSTAMP(3);
+    GSTAMP_FLUSH;
+    if (lane == 0) {
+        st.dw_c = dw_c;
+        st.dc_c = dc_c;
+        A.st[b] = st;
+    }
+    return;
+    }  // PH 1
 
     // ---------------- step, line search with second-order corrections, update
-    direction(rdyn, rin, req);
+    dw_c = st.dw_c;
+    dc_c = st.dc_c;
     double ap, az;
     ftb(ap, az);
     double phi0, th0;
@@ -912,14 +1026,18 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
     }
     const double Dphi = gdot - nu * th0, m0 = phi0 + nu * th0;
     const double slack_m = 10.0 * 2.220446049250313e-16 * fabs(m0);
+    GSTAMP(4);
     double alpha = ap;
     bool accepted = false;
     int soc_used = 0;
     for (int ls = 0; ls < 40; ls++) {
+        GSTAMP(7);
         trial(alpha);
         double ph, th;
         bool okk;
         merit(tx, tu, ts, false, trdyn, trin, treq, ph, th, okk);
+        GSTAMP_COUNT(21, 1);
+        GSTAMP(5);
         const double mt = ph + nu * th;
         if (okk && isfinite(mt) && mt - m0 <= eta * alpha * fmin(Dphi, 0.0) + slack_m) { accepted = true; break; }
         if (ls == 0 && P.max_soc > 0 && (!okk || th >= th0)) {
@@ -930,6 +1048,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
             for (int e = lane; e < N * NET; e += 64) seq[e] = alpha * req[e] + treq[e];
             gsync();
             for (int p = 0; p < P.max_soc; p++) {
+                GSTAMP_COUNT(22, 1);
                 dir_copy(true);
                 direction(sdyn, sin_, seq);
                 double aps, azs;
@@ -954,6 +1073,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
                 for (int e = lane; e < N * NET; e += 64) seq[e] = aps * seq[e] + treq[e];
                 gsync();
             }
+            GSTAMP(15);
             if (accepted) break;
         }
         alpha *= 0.5;
@@ -965,6 +1085,7 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         st.consec_fail = 0;
     }
     st.n_soc += soc_used;
+    GSTAMP(6);
     for (int e = lane; e < (N + 1) * NX; e += 64) x[e] += alpha * dx[e];
     for (int e = lane; e < N * NU; e += 64) u[e] += alpha * du[e];
     for (int e = lane; e < N * NIA; e += 64) { s[e] += alpha * ds[e]; yi[e] += alpha * dyi[e]; }
@@ -990,12 +1111,30 @@ __global__ __launch_bounds__(64) void k_giter(const DevModel *M0, const DevModel
         if (gb(clo[e])) zupd(vL[i], dvL[i], s[i] - clo[e]);
         if (gb(chi[e])) zupd(vU[i], dvU[i], chi[e] - s[i]);
     }
+    GSTAMP(7);
+    GSTAMP_FLUSH;
     if (lane == 0) {
         st.iter++;
         st.mu = mu;
         st.nu = nu;
         A.st[b] = st;
     }
+}
+
+template <class FAM>
+__global__ __launch_bounds__(64) void k_gpre(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                             const DevFrame *F1, GParams P, GArrays A, int batch) {
+    giter_phase<FAM, 0>(M0, M1, F0, F1, P, A, batch);
+}
+template <class FAM>
+__global__ __launch_bounds__(64) void k_gkkt(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                             const DevFrame *F1, GParams P, GArrays A, int batch) {
+    giter_phase<FAM, 1>(M0, M1, F0, F1, P, A, batch);
+}
+template <class FAM>
+__global__ __launch_bounds__(64) void k_gls(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                            const DevFrame *F1, GParams P, GArrays A, int batch) {
+    giter_phase<FAM, 2>(M0, M1, F0, F1, P, A, batch);
 }
 
 // ============================================================== outputs
@@ -1186,7 +1325,9 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     for (int it = 0; it <= P.max_iter && active > 0; it += chunk) {
         for (int c = 0; c < chunk; c++) {
             hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
-            hipLaunchKernelGGL(k_giter<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            hipLaunchKernelGGL(k_gpre<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            hipLaunchKernelGGL(k_gls<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
         }
         GHIPCHK(hipGetLastError());
         GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1442,6 +1583,17 @@ template <class FAM> static int gdual_core(mf_gproblem *p, int b, double *out) {
     out[off] = st.mu;
     return (int)off + 1;
 }
+#ifdef MF_GSTAMPS
+extern "C" int mf_debug_gstamps(unsigned long long *out, int nprob) {
+    if (nprob > 1024) nprob = 1024;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mf::mf_gstamp_buf), sizeof(unsigned long long) * 32 * nprob) == hipSuccess ? 0 : -1;
+}
+extern "C" int mf_debug_gstamps_reset(void) {
+    static unsigned long long z[32 * 1024];
+    return hipMemcpyToSymbol(HIP_SYMBOL(mf::mf_gstamp_buf), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {
     if (!p || !out) return capi_fail(MF_ERR_ARG, "null argument");
     switch (p->kind) {
