@@ -121,6 +121,9 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=0, help="horizons in the CPU sample (0: 4 per thread)")
     ap.add_argument("--cpu-reps", type=int, default=5, help="timed CPU runs (median reported)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1024-shard and single-problem figures")
+    ap.add_argument("--no-generic", action="store_true",
+                    help="skip the generic-solver figures (BASELINE configs 3 and 4, tools/generic_bench.py)")
+    ap.add_argument("--generic-batch", type=int, default=1024, help="horizons per generic-solver figure")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent steps in flight (own workspace, stream and host thread each)")
     args = ap.parse_args()
@@ -341,6 +344,15 @@ def main() -> int:
         t1, c1 = timed(1, 5)
         result["single_problem"] = {"ms_per_solve": t1 * 1e3, "converged": c1, "iters": int(out["iters"][0].item()),
                                     "note": "horizon 0 of the batch alone, median of 5 (host-polled every 4 iterations)"}
+
+    if world == 1 and not args.no_extra and not args.no_generic:
+        # BASELINE configs 3 (dual-arm shared fatigue budget, N = 100) and 4 (Centauro, N = 50) through the
+        # generic stage-structured solver (csrc/gipm.hip): batches of perturbed starts, GPU vs the host IPM
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from generic_bench import GENERIC_STAGE_CAPS, generic_extra
+        torch.cuda.set_device(dev)
+        result["generic"] = generic_extra(batch=args.generic_batch, sample=2, cpu=not args.no_cpu_baseline,
+                                          stage_caps=GENERIC_STAGE_CAPS)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import pin_np as P

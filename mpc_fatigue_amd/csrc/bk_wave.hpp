@@ -91,7 +91,7 @@ struct BKInertia {
 
 // perm/piv: LDS int arrays of length >= m.
 template <int LD>
-__device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
+__device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
     const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     BKInertia in{0, 0, 0};
@@ -104,9 +104,17 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
         // (ds_bpermute round trips); ties keep the smallest index, like a sequential idamax
         double colmax = 0.0;
         int imax = k;
-        for (int i = k + 1; i < m; i++) {
-            double a = fabs(A[i * LD + k]);
-            if (a > colmax) { colmax = a; imax = i; }
+        if (m <= 64) {
+            // lane i holds |A_ik| of its row; the wave argmax keeps the smallest index among ties and
+            // index k when the column is zero: the result of the sequential strict-> scan below
+            colmax = (lane > k && lane < m) ? fabs(A[lane * LD + k]) : 0.0;
+            imax = (lane > k && lane < m) ? lane : k;
+            wave_argmax(colmax, imax);
+        } else {
+            for (int i = k + 1; i < m; i++) {
+                double a = fabs(A[i * LD + k]);
+                if (a > colmax) { colmax = a; imax = i; }
+            }
         }
         double absakk = fabs(A[k * LD + k]);
         int kstep = 1, kp = k;
@@ -121,8 +129,13 @@ __device__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
             kp = k;
         } else {
             double rowmax = 0.0;
-            for (int j = k; j < m; j++)
-                if (j != imax) rowmax = fmax(rowmax, fabs(A[imax * LD + j]));
+            if (m <= 64) {
+                rowmax = (lane >= k && lane < m && lane != imax) ? fabs(A[imax * LD + lane]) : 0.0;
+                rowmax = wave_max(rowmax);
+            } else {
+                for (int j = k; j < m; j++)
+                    if (j != imax) rowmax = fmax(rowmax, fabs(A[imax * LD + j]));
+            }
             if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
             else if (fabs(A[imax * LD + imax]) >= alpha * rowmax) kp = imax;
             else { kp = imax; kstep = 2; }
@@ -431,7 +444,7 @@ __device__ bool ldl_schur_regs(const double *A, double *B, int nr, BKInertia &in
 // the factor by LDS broadcast; no cross-lane traffic and a single barrier.  The L column t
 // acts on rows >= t + 1, or >= t + 2 when t opens a 2x2 pivot (its partner row belongs to D).
 template <int LD, int NR, int M>
-__device__ void bk_solve_cols(const double *A, const int *perm, const int *piv, double *B, int nr) {
+__device__ __forceinline__ void bk_solve_cols(const double *A, const int *perm, const int *piv, double *B, int nr) {
     const int c = lane_opaque();
     double y[M];
     int pv[M];
@@ -478,10 +491,70 @@ __device__ void bk_solve_cols(const double *A, const int *perm, const int *piv, 
     wave_lds_sync();
 }
 
+// bk_factor_wave with the matrix in registers (lane i holds row i, M <= 64) for the common case
+// where Bunch-Kaufman keeps the natural order: every pivot passes the first test
+// |a_kk| >= alpha max_{i>k} |a_ik| and is non-zero.  The column of step k is broadcast with
+// v_readlane and every lane updates the lower part of its own row, A_ij -= (A_ik / d_k) A_jk for
+// k < j <= i, the same arithmetic in the same order as bk_factor_wave, so the factor (L below
+// the diagonal, D on it; perm = identity, piv = 1) and the inertia are identical.  Returns false,
+// with A, perm and piv untouched, as soon as a pivot would need the pivoted path.
+template <int LD, int M>
+__device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, BKInertia &in) {
+    static_assert(M <= 64, "one row per lane");
+    const int lane = lane_opaque();
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    double a[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) a[j] = A[min(lane, M - 1) * LD + j];
+    int pos = 0, neg = 0;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+        if (ok) {
+            double r[M];
+            double colmax = 0.0;
+#pragma unroll
+            for (int i = k + 1; i < M; i++) {
+                r[i] = readlane_d(a[k], i);
+                colmax = fmax(colmax, fabs(r[i]));
+            }
+            const double d = readlane_d(a[k], k);
+            const double absakk = fabs(d);
+            const bool keep = absakk >= alpha * colmax;
+            if (fmax(absakk, colmax) == 0.0 || !keep) {
+                ok = false;
+            } else {
+                if (d > 0) pos++; else neg++;
+                const double inv = 1.0 / d;
+                if (lane > k && lane < M) {
+                    const double ci = a[k];
+#pragma unroll
+                    for (int j = k + 1; j < M; j++)
+                        if (j <= lane) a[j] = a[j] - (ci * inv) * r[j];
+                    a[k] = ci * inv;
+                }
+            }
+        }
+    }
+    if (!ok) return false;
+    if (lane < M) {
+#pragma unroll
+        for (int j = 0; j < M; j++)
+            if (j <= lane) A[lane * LD + j] = a[j];
+        perm[lane] = lane;
+        piv[lane] = 1;
+    }
+    wave_lds_sync();
+    in.pos = pos;
+    in.neg = neg;
+    in.zero = 0;
+    return true;
+}
+
 // Solve A X = B for nr right-hand sides; B is m x NR (row-major, LD NR) in LDS.
 // Y: LDS scratch m x NR.
 template <int LD, int NR>
-__device__ void bk_solve_wave(const double *A, int m, const int *perm, const int *piv, double *B, int nr, double *Y) {
+__device__ __forceinline__ void bk_solve_wave(const double *A, int m, const int *perm, const int *piv, double *B, int nr, double *Y) {
     const int lane = lane_opaque();
     for (int e = lane; e < m * nr; e += 64) {
         int i = e / nr, c = e % nr;

@@ -94,6 +94,21 @@ __device__ __forceinline__ void gsync() {
     __syncthreads();
 }
 
+// nd contiguous doubles global -> LDS by LDS-DMA (global_load_lds_dword: no VGPR destination, every
+// instruction of the copy in flight at once; the next gsync()'s vmcnt(0) retires them).  Dword granularity:
+// the record fields are only 8-byte aligned.  The LDS destination of one instruction is the wave-uniform
+// base + 4 x lane, so lanes past the end are masked off (they would write beyond the array).
+__device__ __forceinline__ void glds_copy(double *lds, const double *src, int nd) {
+    const int lane = threadIdx.x;
+    const int nw = 2 * nd;
+    const unsigned *s = reinterpret_cast<const unsigned *>(src);
+    unsigned *d = reinterpret_cast<unsigned *>(lds);
+    for (int t = 0; t < nw; t += 64)
+        if (t + lane < nw)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(s + t + lane),
+                                             (__attribute__((address_space(3))) void *)(d + t), 4, 0, 0);
+}
+
 // Diagnostic build only (-DMF_GSTAMPS, libmpcfatigue_gstamps.so): per-phase cycle counts of k_giter
 // accumulated in registers by every lane and added to a debug buffer by lane 0 once per launch
 #ifdef MF_GSTAMPS
@@ -524,13 +539,14 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     auto stage_in = [&](int k, bool withW) {
         const double *rk = R(k);
         const bool en = eqon(k + 1);
-        for (int e = lane; e < NX * NX; e += 64) Ab[e] = rk[D::O_A + e];
-        for (int e = lane; e < NX * NU; e += 64) Bb[e] = rk[D::O_B + e];
-        for (int e = lane; e < NI * NV; e += 64) JIs[e] = rk[D::O_JI + e];
-        for (int e = lane; e < NM * NV; e += 64) JMs[e] = rk[D::O_JM + e];
-        if (withW)
-            for (int e = lane; e < NV * NV; e += 64) Hs[e] = rk[D::O_W + e];
-        for (int e = lane; e < NEA * NX; e += 64) Jn[e] = (en && e < NE * NX) ? R(k + 1)[D::O_JE + e] : 0.0;
+        glds_copy(Ab, rk + D::O_A, NX * NX);
+        glds_copy(Bb, rk + D::O_B, NX * NU);
+        if (NI > 0) glds_copy(JIs, rk + D::O_JI, NI * NV);
+        if (NM > 0) glds_copy(JMs, rk + D::O_JM, NM * NV);
+        if (withW) glds_copy(Hs, rk + D::O_W, NV * NV);
+        if (en && NE > 0) glds_copy(Jn, R(k + 1) + D::O_JE, NE * NX);
+        for (int e = lane; e < NEA * NX; e += 64)
+            if (!(en && e < NE * NX)) Jn[e] = 0.0;
         for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
         for (int q = lane; q < NI; q += 64) acts[q] = cact(k, q) ? 1 : 0;
     };
@@ -622,7 +638,10 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 [&](int l, int j) { return T2[l * NX + j]; }, [&](int i, int j, double v) { Qxx[i * NX + j] = v; });
             __syncthreads();
             GSTAMP(11);
-            const BKInertia in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+            // natural-order pivots in registers (the common case), the pivoted LDS factorisation otherwise
+            BKInertia in;
+            // (stage blocks with at most two constraint rows: with more, the Schur rows usually need pivoting)
+            if (!(NET <= 2 && bk_factor_regs<LDK, NK>(Ks, perm, piv, in))) in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
             GSTAMP(12);
             if (in.zero) return 2;
             if (in.pos != NU || in.neg != NET) return 1;
@@ -660,34 +679,37 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         for (int k = N - 1; k >= 0; k--) {
             const double *rk = R(k);
             const bool en = eqon(k + 1);
+            GSTAMP(26);
             for (int j = lane; j < NX; j += 64) pvg[k * NX + j] = pvs[j];
             // every operand of the stage into LDS in one round trip: the record parts, P_{k+1} (T2),
             // the stored stage factorisation (Ks, perm, piv) and feedback (Kf), the stage vectors
             stage_in(k, false);
             {
                 const double *kst = Kg + (size_t)k * KSTG;
-                for (int e = lane; e < NX * NX; e += 64) T2[e] = Pg[(size_t)k * NX * NX + e];
-                for (int e = lane; e < NK * LDK; e += 64) Ks[e] = kst[e];
+                glds_copy(T2, Pg + (size_t)k * NX * NX, NX * NX);
+                glds_copy(Ks, kst, NK * LDK);
+                glds_copy(Kf, Fg + (size_t)k * NK * NX, NK * NX);
+                glds_copy(Vs + V_GL, rk + D::O_GL, NV);
+                glds_copy(Vs + V_GX, gx + k * NX, NX);
+                glds_copy(Vs + V_LK, lam + k * NX, NX);
+                glds_copy(Vs + V_RD, rd + k * NX, NX);
+                glds_copy(Vs + V_GU, gu + k * NU, NU);
+                glds_copy(Vs + V_YE, ye + k * NET, NET);
+                glds_copy(Vs + V_RE, re + k * NET, NET);
+                if (k > 0) glds_copy(Vs + V_LP, lam + (k - 1) * NX, NX);
+                if (k + 1 < N) glds_copy(Vs + V_RN, re + (k + 1) * NET, NEA);
+                if (eqon(k) && NE > 0) glds_copy(Vs + V_JE, rk + D::O_JE, NE * NX);
                 for (int e = lane; e < NK; e += 64) {
                     perm[e] = (int)kst[NK * LDK + e];
                     piv[e] = (int)kst[NK * LDK + NK + e];
                 }
-                for (int e = lane; e < NK * NX; e += 64) Kf[e] = Fg[(size_t)k * NK * NX + e];
             }
-            for (int a = lane; a < NV; a += 64) Vs[V_GL + a] = rk[D::O_GL + a];
-            for (int j = lane; j < NX; j += 64) {
-                Vs[V_GX + j] = gx[k * NX + j];
-                Vs[V_LK + j] = lam[k * NX + j];
-                Vs[V_LP + j] = k > 0 ? lam[(k - 1) * NX + j] : 0.0;
-                Vs[V_RD + j] = rd[k * NX + j];
-            }
-            for (int c = lane; c < NU; c += 64) Vs[V_GU + c] = gu[k * NU + c];
-            for (int ee = lane; ee < NET; ee += 64) {
-                Vs[V_YE + ee] = ye[k * NET + ee];
-                Vs[V_RE + ee] = re[k * NET + ee];
-            }
-            for (int ee = lane; ee < NEA; ee += 64) Vs[V_RN + ee] = (k + 1 < N) ? re[(k + 1) * NET + ee] : 0.0;
-            for (int e = lane; e < NEA * NX; e += 64) Vs[V_JE + e] = (eqon(k) && e < NE * NX) ? rk[D::O_JE + e] : 0.0;
+            for (int j = lane; j < NX; j += 64)
+                if (k == 0) Vs[V_LP + j] = 0.0;
+            for (int ee = lane; ee < NEA; ee += 64)
+                if (k + 1 >= N) Vs[V_RN + ee] = 0.0;
+            for (int e = lane; e < NEA * NX; e += 64)
+                if (!(eqon(k) && e < NE * NX)) Vs[V_JE + e] = 0.0;
             // slack-row weights of the stage (vx: the J_I^T w term)
             for (int q = lane; q < NI; q += 64) {
                 const int i = k * NIA + q;
@@ -699,6 +721,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 Vs[V_W + q] = w;
             }
             gsync();
+            GSTAMP(19);
             for (int a = lane; a < NV; a += 64) {
                 const bool fa = a < NX ? (k == 0) : fixs[a - NX];
                 double g = 0.0;
@@ -724,6 +747,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 tv[j] = acc;
             }
             gsync();
+            GSTAMP(23);
             for (int a = lane; a < NK; a += 64) {
                 double z = 0.0;
                 if (a < NU) {
@@ -742,8 +766,11 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 duv[a] = -z;
             }
             wave_lds_sync();
-            bk_solve_wave<LDK, 1>(Ks, NK, perm, piv, duv, 1, Ys);
+            GSTAMP(24);
+            if constexpr (NK <= 24 && PH == 1) bk_solve_cols<LDK, 1, NK>(Ks, perm, piv, duv, 1);  // (k_gls: register budget)
+            else bk_solve_wave<LDK, 1>(Ks, NK, perm, piv, duv, 1, Ys);
             for (int a = lane; a < NK; a += 64) kvg[k * NK + a] = duv[a];
+            GSTAMP(25);
             if (k > 0)
                 for (int j = lane; j < NX; j += 64) {
                     double acc = vx[j];
@@ -753,6 +780,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 }
             gsync();
         }
+        GSTAMP(26);
         // forward sweep
         for (int j = lane; j < NX; j += 64) { dxs[j] = 0.0; dx[j] = 0.0; }
         for (int ee = lane; ee < NEA; ee += 64) dye[ee] = 0.0;  // state rows of node 0 (inactive)
@@ -761,13 +789,17 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             const double *rk = R(k);
             const bool en = eqon(k + 1);
             // the stage's operands into LDS first (one round trip), then three LDS-only phases
-            for (int e = lane; e < NX * NX; e += 64) { Ab[e] = rk[D::O_A + e]; T2[e] = Pg[(size_t)k * NX * NX + e]; }
-            for (int e = lane; e < NX * NU; e += 64) Bb[e] = rk[D::O_B + e];
-            for (int e = lane; e < NK * NX; e += 64) Kf[e] = Fg[(size_t)k * NK * NX + e];
-            for (int e = lane; e < NEA * NX; e += 64) Jn[e] = (en && e < NE * NX) ? R(k + 1)[D::O_JE + e] : 0.0;
-            for (int a = lane; a < NK; a += 64) zv[a] = kvg[k * NK + a];
+            glds_copy(Ab, rk + D::O_A, NX * NX);
+            glds_copy(T2, Pg + (size_t)k * NX * NX, NX * NX);
+            glds_copy(Bb, rk + D::O_B, NX * NU);
+            glds_copy(Kf, Fg + (size_t)k * NK * NX, NK * NX);
+            if (en && NE > 0) glds_copy(Jn, R(k + 1) + D::O_JE, NE * NX);
+            glds_copy(zv, kvg + k * NK, NK);
+            glds_copy(tv, pvg + k * NX, NX);
+            glds_copy(vx, rd + k * NX, NX);
+            for (int e = lane; e < NEA * NX; e += 64)
+                if (!(en && e < NE * NX)) Jn[e] = 0.0;
             for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
-            for (int j = lane; j < NX; j += 64) { tv[j] = pvg[k * NX + j]; vx[j] = rd[k * NX + j]; }
             gsync();
             for (int a = lane; a < NK; a += 64) {
                 double acc = zv[a];
@@ -799,6 +831,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             for (int j = lane; j < NX; j += 64) dxs[j] = dxn[j];
             gsync();
         }
+        GSTAMP(17);
         // slack rows and bound multipliers
         for (int e = lane; e < N * NI; e += 64) {
             const int k = e / NI, q = e % NI, i = k * NIA + q;
@@ -844,6 +877,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             dvU[i] = c;
         }
         gsync();
+        GSTAMP(18);
     };
 
     auto ftb = [&](double &ap_o, double &az_o) {

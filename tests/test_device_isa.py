@@ -1,0 +1,49 @@
+"""Device-code guard (CPU): the gfx950 code objects inside libmpcfatigue.so contain no device function calls.
+
+Every kernel is one inlined body: a non-inlined device call (s_swappc_b64) passes its LDS arrays as flat pointers
+and keeps its locals in a scratch stack frame.  The only GPU fault of round 3 came from exactly that (the
+generic solver's line-search kernel calling a register-array triangular solve the inliner had declined: an
+aperture violation), so the heavy device routines are __forceinline__ and this test keeps it so.
+The code objects are read from the clang offload bundles of the shared object (no GPU needed).
+"""
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "mpc_fatigue_amd", "libmpcfatigue.so")
+OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+def _gfx950_objects(path):
+    b = open(path, "rb").read()
+    out = []
+    for m in re.finditer(re.escape(b"__CLANG_OFFLOAD_BUNDLE__"), b):
+        st = m.start()
+        n = struct.unpack_from("<Q", b, st + 24)[0]
+        p = st + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", b, p)
+            p += 24
+            triple = b[p:p + tl].decode()
+            p += tl
+            if "gfx950" in triple and size > 0:
+                out.append(b[st + off:st + off + size])
+    return out
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump missing")
+def test_no_device_function_calls(tmp_path):
+    objs = _gfx950_objects(LIB)
+    assert objs, "no gfx950 code object in libmpcfatigue.so"
+    calls = 0
+    for i, o in enumerate(objs):
+        f = tmp_path / f"co{i}.o"
+        f.write_bytes(o)
+        asm = subprocess.run([OBJDUMP, "-d", str(f)], capture_output=True, text=True, check=True).stdout
+        assert "s_endpgm" in asm
+        calls += asm.count("s_swappc_b64")
+    assert calls == 0, f"{calls} device function calls (s_swappc_b64) in the gfx950 code objects"

@@ -3,7 +3,8 @@ mpc_fatigue_amd/libmpcfatigue_gstamps.so, `make -C mpc_fatigue_amd libmpcfatigue
 
 Usage: python tools/gdiag_stamps.py [batch] [iters] [case]    case: c3 (shared budget, pos_toll 1) | c4
 Slots: 0 opt-error+mu, 1 barrier/residuals, 2 factor rest, 8 stage loads, 9 H assembly, 10 PB / PA,
-11 stage block, 12 BK factor, 13 BK solve + stores, 14 P update, 3 direction, 4 ftb+merit0+gdot/pHp,
+11 stage block, 12 BK factor, 13 BK solve + stores, 14 P update; direction (both calls): 19 stage loads,
+23 vx / tv, 24 zv, 25 solve, 26 pvs and loop top, 17 forward sweep, 18 slack rows and bound multipliers; 3 rest, 4 ftb+merit0+gdot/pHp,
 5 trial merits, 15 second-order corrections, 6 after the line search, 7 update; counters 20 factorisation
 tries, 21 trial merits, 22 SOC directions.
 """
@@ -45,10 +46,10 @@ buf = (C.c_ulonglong * (32 * n))()
 L.mf_debug_gstamps(buf, n)
 a = np.array(buf, dtype=np.float64).reshape(n, 32)
 it = np.maximum(res.iters[:n], 1).astype(float)
-cols = [0, 1, 8, 9, 10, 11, 12, 13, 14, 2, 3, 4, 5, 15, 6, 7]
+cols = [0, 1, 8, 9, 10, 11, 12, 13, 14, 2, 19, 23, 24, 25, 26, 17, 18, 3, 4, 5, 15, 6, 7]
 names = ["opt-err+mu", "barrier+resid", " f:stage loads", " f:H assembly", " f:PB,PA", " f:stage block", " f:BK factor",
-         " f:BK solve+st", " f:P update", " f:rest", "direction", "ftb+merit0+pHp", "trial merits", "SOC", "post-LS",
-         "update"]
+         " f:BK solve+st", " f:P update", " f:rest", " d:stage loads", " d:vx,tv", " d:zv", " d:solve", " d:pvs+loop",
+         " d:forward", " d:tail", "direction rest", "ftb+merit0+pHp", "trial merits", "SOC rest", "post-LS", "update"]
 tot = a[:, cols].sum(1)
 print(f"{case} batch {B}: status", {int(s): int((res.status == s).sum()) for s in np.unique(res.status)},
       "mean iters", res.iters.mean())

@@ -26,6 +26,12 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# iteration caps of the C3 homotopy stages in the bench figure (pos_toll 1, 1e-2, 1e-4): the intermediate stages only
+# carry the iterate along the homotopy (their end points warm-start the next stage); the last stage is the reference
+# problem with the full 1000-iteration cap
+GENERIC_STAGE_CAPS = [150, 300, 1000]
+
+
 def _golden_q0():
     g = np.loadtxt(os.path.join(ROOT, "tests", "golden", "G1_box_N50_solution.csv"), delimiter=",")
     return g[:12]
@@ -36,7 +42,9 @@ def _x_traj(w, nx, nu, N):
     return np.concatenate([w[:, None, :nx], w[:, nx:].reshape(w.shape[0], N, nu + nx)[:, :, nu:]], axis=1)
 
 
-def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0, cases=("c3", "c4")) -> dict:
+def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0, cases=("c3", "c4"),
+                  stage_caps=None, batch_c4: int | None = None) -> dict:
+    """stage_caps: iteration caps of the C3 homotopy stages (default: 1000 each, GOCP.solve_box's)."""
     import torch
 
     from mpc_fatigue_amd import problems as PR
@@ -55,10 +63,13 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
                   dict(u_init=PR.box_u_init(sp3), max_iter=1000, max_soc=4)))
     sp4 = PR.centauro(N=50, T=2.0)
     q0c = np.asarray(sp4["q0"])
-    X4 = np.hstack([q0c[None] + rng.uniform(-0.02, 0.02, (batch, 14)), np.tile(sp4["T0"], (batch, 1))])
+    b4 = batch_c4 or batch
+    X4 = np.hstack([q0c[None] + rng.uniform(-0.02, 0.02, (b4, 14)), np.tile(sp4["T0"], (b4, 1))])
     cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(u_init=PR.centauro_u_init(sp4), max_iter=500, max_soc=4)))
     cases = [c for c in cases if c[0][:2] in todo]
     for name, spec, X, stages, kw in cases:
+        batch = X.shape[0]
+        caps = list(stage_caps) if (stage_caps and len(stages) > 1) else [kw["max_iter"]] * len(stages)
         gs = [GOCP(st) for st in stages]
         nx, nu, N = gs[0].nx, gs[0].nu, spec["N"]
         x = torch.as_tensor(X, dtype=torch.float64, device=dev).contiguous()
@@ -72,7 +83,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
             prev = None
             for i, (g, ob) in enumerate(zip(gs, bufs)):
                 ptr = {k: v.data_ptr() for k, v in ob.items()}
-                kw2 = dict(kw) if max_iter is None else dict(kw, max_iter=max_iter)
+                kw2 = dict(kw, max_iter=caps[i] if max_iter is None else max_iter)
                 t = time.perf_counter()
                 g.solve_dev(x.data_ptr(), None, None if prev is None else prev.data_ptr(), None, batch, ptr,
                             stream=stream.cuda_stream, **kw2)
@@ -90,7 +101,8 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
         conv = int((st == 0).sum())
         rec = {"value": conv / dt, "unit": "horizons/s", "batch": batch, "converged": conv,
                "converged_frac": conv / batch, "seconds": dt, "stages": len(stages),
-               "mean_iters_per_stage": [i / batch for i in its], "N": N, "nx": nx, "nu": nu, "ni": gs[0].ni}
+               "mean_iters_per_stage": [i / batch for i in its], "stage_max_iter": caps,
+               "N": N, "nx": nx, "nu": nu, "ni": gs[0].ni}
         if cpu and sample > 0:
             from oracle import cpu_fast as CF
             from oracle import generic as G
@@ -124,7 +136,9 @@ if __name__ == "__main__":
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--cases", default="c3,c4", help="comma list of c3 (shared budget N=100) and c4 (Centauro N=50)")
     ap.add_argument("--sample", type=int, default=2)
+    ap.add_argument("--caps", default="", help="comma list of C3 homotopy stage iteration caps (default 1000 each)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
-    print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")))))
+    caps = [int(c) for c in a.caps.split(",")] if a.caps else None
+    print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")), stage_caps=caps)))
