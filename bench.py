@@ -251,12 +251,26 @@ def main() -> int:
     total_bytes = NODE_BYTES * float(node_evals.item()) * timing_steps  # this rank's node evaluations
     bytes_per_launch = total_bytes / max(1, ev_launches)
     achieved = total_bytes / (ev_ms / 1e3) / 1e9
-    traffic, fp64 = None, None
+    traffic, fp64, iter_traffic = None, None, None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc_path):
         with open(pmc_path) as f:
             pmc = json.load(f)
         ev = pmc.get("k_eval_node", {})
+        # whole-iteration HBM traffic (PMC FETCH_SIZE + WRITE_SIZE of every per-iteration kernel, per launch) at the
+        # profiled workload, and per running horizon-iteration (running horizons per launch = node evaluations / N)
+        it_k = ["k_eval_q", "k_eval_node[qd]", "k_eval_asm", "k_ipm_pre", "k_ipm_kkt", "k_kkt_recover", "k_ipm_post",
+                "k_post_update", "k_compact"]
+        it_k = [k for k in it_k if k in pmc]  # (k_post_update: folded into k_ipm_post in round 3)
+        if "k_ipm_kkt" in it_k and ev.get("node_evals"):
+            per_k = {k: pmc[k]["hbm_bytes_per_launch"] for k in it_k}
+            tot = sum(per_k.values())
+            running = ev["node_evals"] / ev["launches"] / N
+            iter_traffic = {"hbm_bytes_per_iteration": tot, "running_horizons_per_iteration": running,
+                            "hbm_bytes_per_horizon_iteration": tot / running,
+                            "eval_algorithmic_bytes_per_horizon_iteration": NODE_BYTES * N,
+                            "per_kernel_bytes_per_iteration": per_k,
+                            "source": "profiles/pmc_traffic.json (PMC of tools/traffic_run.py: the C5 batch solved once)"}
         if ev.get("hbm_bytes_per_node_eval"):
             traffic = ev["hbm_bytes_per_node_eval"] * total_bytes / NODE_BYTES / max(1, ev_launches)
         if ev.get("fp64_flops_per_node_eval"):
@@ -275,6 +289,7 @@ def main() -> int:
         "avg_launch_ms": per_launch_ms, "launches": ev_launches,
         "kernel_ms": {k: v[0] for k, v in stats.items()},
         "kernel_share": {k: v[0] / total_ms for k, v in stats.items()}, "fp64": fp64,
+        "iteration_traffic": iter_traffic,
         "launch_note": ("one k_eval_node launch = the solver's phase 0: k_eval_node<..,0> (q directions) then "
                         "k_eval_node<..,1> (qd directions) on one stream; rocprofv3 lists the two, their averages "
                         "sum to avg_launch_ms. Bytes: SURVEY.md s.8(d) 952 B per running node evaluation"),

@@ -696,7 +696,7 @@ template <int NT> __device__ __forceinline__ double block_sum(double v, double *
 //                   first inertia try's Riccati stage inputs (256-thread block per problem)
 //   k_ipm_kkt     : inertia-corrected Riccati recursion and forward sweep (one wave per problem)
 //   k_kkt_recover : step recovery, fraction to the boundary, merit slope / curvature (block per problem)
-//   k_ipm_post    : merit line search (one wave per problem); k_post_update: the update (block)
+//   k_ipm_post    : merit line search and the primal-dual update (two waves per problem)
 // Scalars that cross a boundary travel in ProbState (mu, nu, tau_fb, regularisation, step bounds,
 // directional derivative and curvature).
 template <int NJ, int NF, int NL, int NT, class Sync>
@@ -1797,7 +1797,7 @@ __global__ __launch_bounds__(64, 3) void k_ipm_kkt(const DevModel *__restrict__ 
 }
 
 template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+__global__ __launch_bounds__(128) void k_ipm_post(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                  OcpConst C, IpmArrays A, int batch) {
     constexpr int n = NJ, nf = NF, nl = NL;
     constexpr int NV = 2 * NJ + NF;
@@ -1807,7 +1807,8 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
     __shared__ ModelLds<NJ> Ml;
     const DevModel &M = Ml.get();
     __shared__ DevFrame F;
-    __shared__ int perm[MB], piv[MB];
+    constexpr int NT = 128;  // two waves per horizon: every node of the merit sweep in one pass (N <= 128)
+    __shared__ double red[8 * (NT / 64)];
     const int lane = threadIdx.x;
     if ((int)blockIdx.x >= *A.nrun) return;
     const int b = A.list[blockIdx.x];
@@ -1853,8 +1854,8 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
     auto finish = [&](int status) {
         STAMP_FLUSH;
         double f = 0.0;
-        for (int k = lane; k < N; k += 64) f += cost[k];
-        f = wave_sum(f);
+        for (int k = lane; k < N; k += NT) f += cost[k];
+        f = block_sum<NT>(f, red);
         if (lane == 0) {
             st.status = status;
             st.obj = f;
@@ -1877,7 +1878,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         double f = 0, bar = 0, th = 0, pm = 1.0;  // barrier: -log of the gaps' product, renormalised per element
         int pe = 0, pe_ = 0;
         int bad = 0;
-        for (int k = lane; k < N; k += 64) {
+        for (int k = lane; k < N; k += NT) {
             // only the sweep's inputs are held through the sweep; slacks, bounds and q_{k+1} are
             // read after it (register budget of the sweep)
             double tq[NJ], tqd[NJ], tv[NJ], Fw[3], c = 0.0;
@@ -1922,11 +1923,11 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
             f += c;
             th += mo.th;
         }
-        for (int e0 = lane; e0 < N * n; e0 += 64 * UB) {
+        for (int e0 = lane; e0 < N * n; e0 += NT * UB) {
             double xq[UB], xd[UB], xs[UB], lo[UB], hi[UB];
 #pragma unroll
             for (int u = 0; u < UB; u++) {
-                const int e = min(e0 + 64 * u, N * n - 1);
+                const int e = min(e0 + NT * u, N * n - 1);
                 xq[u] = q[e + n] + alpha * dq[e + n];
                 xd[u] = qd[e] + alpha * dqd[e];
                 xs[u] = s[e] + alpha * ds[e];
@@ -1935,7 +1936,7 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
             }
 #pragma unroll
             for (int u = 0; u < UB; u++) {
-                const int e = e0 + 64 * u;
+                const int e = e0 + NT * u;
                 if (e < N * n) {
                     const int k = e / n, j = e % n;
                     if (hasb(QLO[j])) { if (xq[u] - QLO[j] <= 0) bad = 1; else pm *= xq[u] - QLO[j]; }
@@ -1952,8 +1953,12 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
             }
         }
         bar = -(log(pm) + pe * 0.69314718055994530942);
-        f = wave_sum(f); bar = wave_sum(bar); th = wave_sum(th);
-        bad = wave_sum_i(bad);
+        {
+            double sm[4] = {f, bar, th, (double)bad};
+            block_reduce<NT, 0, 4>(nullptr, sm, red);
+            f = sm[0]; bar = sm[1]; th = sm[2];
+            bad = sm[3] != 0.0 ? 1 : 0;
+        }
         phi = f + mu * bar;
         theta = th;
         ok_out = (bad == 0);
@@ -1996,10 +2001,75 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
         st.consec_fail = 0;
     }
 
-    st.alpha = alpha;  // the update itself: k_post_update (a block per horizon)
+    st.alpha = alpha;
     STAMP(6);
     STAMP_COUNT(10, 1);
     STAMP_FLUSH;
+    // ---------------- update: the primal-dual step with alpha, the bound multipliers with az and the new
+    // slacks (formerly the k_post_update launch: the same element loops, now by this block's 128 threads)
+    __syncthreads();  // every merit sweep has read the iterate
+    {
+        auto zupd = [&](double z, double dz, double slack) {
+            const double zz = z + az * dz;
+            return fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
+        };
+        for (int e0 = lane; e0 < (N + 1) * n; e0 += NT * UB) {
+            double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB];
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = min(e0 + NT * u, (N + 1) * n - 1);
+                x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; dzl[u] = dzqL[e]; zu[u] = zqU[e]; dzu[u] = dzqU[e];
+            }
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = e0 + NT * u;
+                if (e < (N + 1) * n) {
+                    const int j = e % n;
+                    const double xn = x[u] + alpha * dx[u];
+                    q[e] = xn;
+                    if (e >= n) {
+                        if (hasb(QLO[j])) zqL[e] = zupd(zl[u], dzl[u], xn - QLO[j]);
+                        if (hasb(QHI[j])) zqU[e] = zupd(zu[u], dzu[u], QHI[j] - xn);
+                    }
+                }
+            }
+        }
+        for (int e0 = lane; e0 < N * n; e0 += NT * UB) {
+            double x[UB], xs[UB], zl[UB], zu[UB], vl[UB], vu[UB], lo[UB], hi[UB], yn[UB], dn[UB];
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = min(e0 + NT * u, N * n - 1);
+                x[u] = qd[e] + alpha * dqd[e];
+                xs[u] = s[e] + alpha * ds[e];
+                yn[u] = yc[e] + alpha * dyc[e];
+                dn[u] = yd[e] + alpha * dyd[e];
+                zl[u] = zdL[e] + az * dzdL[e]; zu[u] = zdU[e] + az * dzdU[e];
+                vl[u] = vL[e] + az * dvL[e]; vu[u] = vU[e] + az * dvU[e];
+                lo[u] = tlo[e]; hi[u] = thi[e];
+            }
+            auto clampz = [&](double zz, double slack) {
+                return fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
+            };
+#pragma unroll
+            for (int u = 0; u < UB; u++) {
+                const int e = e0 + NT * u;
+                if (e < N * n) {
+                    const int k = e / n, j = e % n;
+                    qd[e] = x[u]; s[e] = xs[u]; yc[e] = yn[u]; yd[e] = dn[u];
+                    if (k > 0) {
+                        if (hasb(DLO[j])) zdL[e] = clampz(zl[u], x[u] - DLO[j]);
+                        if (hasb(DHI[j])) zdU[e] = clampz(zu[u], DHI[j] - x[u]);
+                    }
+                    if (hasb(lo[u])) vL[e] = clampz(vl[u], xs[u] - lo[u]);
+                    if (hasb(hi[u])) vU[e] = clampz(vu[u], hi[u] - xs[u]);
+                }
+            }
+        }
+        if constexpr (NF > 0)
+            for (int e = lane; e < N * nf; e += NT) Fv[(e / nf) * NFA + e % nf] += alpha * dF[(e / nf) * NFA + e % nf];
+        if constexpr (NL > 0)
+            for (int e = lane; e < N * nl; e += NT) yl[e] += alpha * dyl[e];
+    }
     if (lane == 0) {
         st.iter++;
         st.mu = mu;
@@ -2009,100 +2079,6 @@ __global__ __launch_bounds__(64, 2) void k_ipm_post(const DevModel *__restrict__
 #undef TACT
 }
 
-
-// The primal-dual update with the step k_ipm_post accepted (alpha) and the bound multipliers' step
-// az, one 256-thread block per running horizon.
-template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(256) void k_post_update(OcpConst C, IpmArrays A, int batch) {
-    constexpr int n = NJ, nf = NF, nl = NL;
-    constexpr int NFA = NF > 0 ? NF : 1;
-    constexpr int NT = 256, UB = 2;
-    if ((int)blockIdx.x >= *A.nrun) return;
-    const int b = A.list[blockIdx.x];
-    const ProbState st = A.st[b];
-    if (st.status != ST_RUNNING) return;
-    const int tid = threadIdx.x;
-    __shared__ double Bnd[4 * NJ];
-    if (tid < NJ) {
-        Bnd[tid] = C.q_lo[tid];
-        Bnd[NJ + tid] = C.q_hi[tid];
-        Bnd[2 * NJ + tid] = C.qd_lo[tid];
-        Bnd[3 * NJ + tid] = C.qd_hi[tid];
-    }
-    __syncthreads();
-    const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
-    const IpmSizes S = ipm_sizes(C);
-    const int N = C.N;
-    const double mu = st.mu, alpha = st.alpha, az = st.az, kappa_sigma = 1e10;
-    double *q = A.q + b * S.q, *qd = A.qd + b * S.u, *Fv = A.F + b * S.f, *s = A.s + b * S.u;
-    double *yc = A.yc + b * S.u, *yl = A.yl + b * S.l, *yd = A.yd + b * S.u;
-    double *zqL = A.zqL + b * S.q, *zqU = A.zqU + b * S.q, *zdL = A.zdL + b * S.u, *zdU = A.zdU + b * S.u;
-    double *vL = A.vL + b * S.u, *vU = A.vU + b * S.u;
-    const double *dq = A.dq + b * S.q, *dqd = A.dqd + b * S.u, *dF = A.dF + b * S.f, *ds = A.ds + b * S.u;
-    const double *dyc = A.dyc + b * S.u, *dyl = A.dyl + b * S.l, *dyd = A.dyd + b * S.u;
-    const double *dzqL = A.dzqL + b * S.q, *dzqU = A.dzqU + b * S.q, *dzdL = A.dzdL + b * S.u, *dzdU = A.dzdU + b * S.u;
-    const double *dvL = A.dvL + b * S.u, *dvU = A.dvU + b * S.u;
-    const double *tlo = A.tau_lo, *thi = A.tau_hi;
-    // ---------------- update (primal-dual step, then the bound multipliers with the new slacks)
-    auto zupd = [&](double z, double dz, double slack) {
-        const double zz = z + az * dz;
-        return fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
-    };
-    for (int e0 = tid; e0 < (N + 1) * n; e0 += NT * UB) {
-        double x[UB], dx[UB], zl[UB], dzl[UB], zu[UB], dzu[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + NT * u, (N + 1) * n - 1);
-            x[u] = q[e]; dx[u] = dq[e]; zl[u] = zqL[e]; dzl[u] = dzqL[e]; zu[u] = zqU[e]; dzu[u] = dzqU[e];
-        }
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = e0 + NT * u;
-            if (e < (N + 1) * n) {
-                const int j = e % n;
-                const double xn = x[u] + alpha * dx[u];
-                q[e] = xn;
-                if (e >= n) {
-                    if (hasb(QLO[j])) zqL[e] = zupd(zl[u], dzl[u], xn - QLO[j]);
-                    if (hasb(QHI[j])) zqU[e] = zupd(zu[u], dzu[u], QHI[j] - xn);
-                }
-            }
-        }
-    }
-    for (int e0 = tid; e0 < N * n; e0 += NT * UB) {
-        double x[UB], xs[UB], zl[UB], zu[UB], vl[UB], vu[UB], lo[UB], hi[UB], yn[UB], dn[UB];
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = min(e0 + NT * u, N * n - 1);
-            x[u] = qd[e] + alpha * dqd[e];
-            xs[u] = s[e] + alpha * ds[e];
-            yn[u] = yc[e] + alpha * dyc[e];
-            dn[u] = yd[e] + alpha * dyd[e];
-            zl[u] = zdL[e] + az * dzdL[e]; zu[u] = zdU[e] + az * dzdU[e];
-            vl[u] = vL[e] + az * dvL[e]; vu[u] = vU[e] + az * dvU[e];
-            lo[u] = tlo[e]; hi[u] = thi[e];
-        }
-        auto clampz = [&](double zz, double slack) {
-            return fmax(fmin(zz, kappa_sigma * mu / slack), mu / (kappa_sigma * slack));
-        };
-#pragma unroll
-        for (int u = 0; u < UB; u++) {
-            const int e = e0 + NT * u;
-            if (e < N * n) {
-                const int k = e / n, j = e % n;
-                qd[e] = x[u]; s[e] = xs[u]; yc[e] = yn[u]; yd[e] = dn[u];
-                if (k > 0) {
-                    if (hasb(DLO[j])) zdL[e] = clampz(zl[u], x[u] - DLO[j]);
-                    if (hasb(DHI[j])) zdU[e] = clampz(zu[u], DHI[j] - x[u]);
-                }
-                if (hasb(lo[u])) vL[e] = clampz(vl[u], xs[u] - lo[u]);
-                if (hasb(hi[u])) vU[e] = clampz(vu[u], hi[u] - xs[u]);
-            }
-        }
-    }
-    for (int e = tid; e < N * nf; e += NT) Fv[(e / nf) * NFA + e % nf] += alpha * dF[(e / nf) * NFA + e % nf];
-    for (int e = tid; e < N * nl; e += NT) yl[e] += alpha * dyl[e];
-}
 
 // ============================================================== output in the reference layout
 template <int NJ, int NF>
@@ -2199,8 +2175,7 @@ struct IpmLaunch {
             hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
             hipLaunchKernelGGL((k_kkt_recover<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
         } else {
-            hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
-            hipLaunchKernelGGL((k_post_update<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
+            hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(nact), dim3(128), 0, s, M, F, C, A, batch);
             hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, A, batch);
         }
     }
