@@ -1109,31 +1109,23 @@ __device__ __forceinline__ void kkt_first_try(const ProbState &st, int &tier, do
     dFr = (tier == 1) ? reg : 0.0;
 }
 
-// Step recovery after k_ipm_kkt's sweeps, one 256-thread block per running horizon:
+// Step recovery after k_ipm_kkt's sweeps:
 // dyc_k = P_{k+1} dx_{k+1} + p_{k+1} + Jl_{k+1}^T dyl_{k+1} for every stage, dyd, ds, the bound
-// multiplier steps and the step-curvature correction pcorr (-> k_ipm_post).
-template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, int batch) {
+// multiplier steps and the step-curvature correction pcorr.
+// Step recovery of one horizon by the NT threads of its block (the first part of k_ipm_post since round 3;
+// formerly its own launch): dy_c, dy_tau, ds, the bound-multiplier steps, the fraction to the boundary,
+// grad(phi)^T dx, dx^T (W + Sigma) dx and the merit at the iterate.  Bnd: q_lo, q_hi, qd_lo, qd_hi in LDS;
+// red: >= 7 NT / 64 doubles of LDS.  out = {ap, az, gdot, pHp, phi0, th0}, the same in every thread.
+template <int NJ, int NF, int NL, int NT>
+__device__ __forceinline__ void kkt_recover_body(const OcpConst &C, const IpmArrays &A, int b, const ProbState &st,
+                                                 const double *Bnd, double *red, double *out) {
     constexpr int n = NJ, nl = NL;
     constexpr int NV = 2 * NJ + NF;
     constexpr int NFA = NF > 0 ? NF : 1;
     constexpr int MB = 3 * NJ + NF + NL;
     constexpr int NU = NJ + NF;
-    constexpr int NT = 256, UB = 2;
-    if ((int)blockIdx.x >= *A.nrun) return;
-    const int b = A.list[blockIdx.x];
-    const ProbState st = A.st[b];
-    if (st.status != ST_RUNNING) return;
+    constexpr int UB = 2;
     const int tid = threadIdx.x;
-    __shared__ double Bnd[4 * NJ];
-    __shared__ double red[7 * (NT / 64)];
-    if (tid < NJ) {
-        Bnd[tid] = C.q_lo[tid];
-        Bnd[NJ + tid] = C.q_hi[tid];
-        Bnd[2 * NJ + tid] = C.qd_lo[tid];
-        Bnd[3 * NJ + tid] = C.qd_hi[tid];
-    }
-    __syncthreads();
     const double *QLO = Bnd, *QHI = Bnd + NJ, *DLO = Bnd + 2 * NJ, *DHI = Bnd + 3 * NJ;
     const IpmSizes S = ipm_sizes(C);
     const int N = C.N;
@@ -1356,14 +1348,12 @@ __global__ __launch_bounds__(256) void k_kkt_recover(OcpConst C, IpmArrays A, in
     bar0 = -(log(pm) + pe * 0.69314718055994530942);
     double mx[2] = {-ap, -az}, sm[5] = {gdot, pHp, f0, bar0, th0};
     block_reduce<NT, 2, 5>(mx, sm, red);
-    if (tid == 0) {
-        A.st[b].ap = -mx[0];
-        A.st[b].az = -mx[1];
-        A.st[b].gdot = sm[0];
-        A.st[b].pHp = sm[1];
-        A.st[b].phi0 = sm[2] + mu * sm[3];
-        A.st[b].th0 = sm[4];
-    }
+    out[0] = -mx[0];
+    out[1] = -mx[1];
+    out[2] = sm[0];
+    out[3] = sm[1];
+    out[4] = sm[2] + mu * sm[3];
+    out[5] = sm[4];
 }
 
 template <int NJ, int NF, int NL>
@@ -1866,8 +1856,13 @@ __global__ __launch_bounds__(128) void k_ipm_post(const DevModel *__restrict__ M
         }
     };
     const double tau_fb = st.tau_fb;
-    // ---------------- fraction to boundary (k_kkt_recover)
-    const double ap = st.ap, az = st.az;
+    // ---------------- step recovery, fraction to the boundary, merit slope and curvature (kkt_recover_body)
+    double rcv[6];
+    kkt_recover_body<NJ, NF, NL, NT>(C, A, b, st, Bnd, red, rcv);
+    __syncthreads();  // the recovered steps (ds, dy, dz, dv) are read by other threads below
+    const double ap = rcv[0], az = rcv[1];
+    st.ap = ap;
+    st.az = az;
     TRACE(9, ap); TRACE(10, az);
 
     // ---------------- merit at the current point, directional derivative, curvature
@@ -1965,9 +1960,9 @@ __global__ __launch_bounds__(128) void k_ipm_post(const DevModel *__restrict__ M
     };
     // merit at the current point from this iteration's node evaluation (k_kkt_recover); it equals the
     // value sweep at alpha = 0 to round-off, which the acceptance test's 10 eps |m0| allowance covers
-    const double phi0 = st.phi0, th0 = st.th0;
+    const double phi0 = rcv[4], th0 = rcv[5];
     // gdot = grad(phi)^T dx, pHp = dx^T (W + Sigma) dx (k_kkt_recover)
-    const double gdot = st.gdot, pHp = st.pHp;
+    const double gdot = rcv[2], pHp = rcv[3];
     if (th0 > 1e-300) {
         double nreq = (gdot + 0.5 * fmax(pHp, 0.0)) / ((1.0 - rho) * th0);
         if (nu < nreq) nu = nreq + 1.0;
@@ -2173,7 +2168,6 @@ struct IpmLaunch {
             hipLaunchKernelGGL((k_ipm_pre<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, M, F, C, A, batch);
         } else if (phase == 3) {
             hipLaunchKernelGGL((k_ipm_kkt<NJ, NF, NL>), dim3(nact), dim3(64), 0, s, M, F, C, A, batch);
-            hipLaunchKernelGGL((k_kkt_recover<NJ, NF, NL>), dim3(nact), dim3(256), 0, s, C, A, batch);
         } else {
             hipLaunchKernelGGL((k_ipm_post<NJ, NF, NL>), dim3(nact), dim3(128), 0, s, M, F, C, A, batch);
             hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, A, batch);
