@@ -109,23 +109,25 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
             fk = CF.FastNodes(spec)
             w = None
             t1 = time.perf_counter()
-            for st_spec in stages:
+            # the same stages and caps on one host thread per horizon, with the GPU's KKT algorithm (the Riccati
+            # recursion, mfg_opts.riccati) and the product's node functions built for the host
+            for st_spec, cap in zip(stages, caps):
                 specs = [dict(st_spec, q0=list(X[i, :len(spec["q0"])]), T0=list(X[i, len(spec["q0"]):]))
                          for i in range(sample)]
-                kwc = dict(kw, **fk.opts_kw())
-                if w is not None:
-                    res = [G.solve_batch([s], L=CF.lib(), w0=w[i], **kwc) for i, s in enumerate(specs)]
-                    w = np.vstack([r[0] for r in res])
-                    R = [r[1][0] for r in res]
-                else:
-                    w, R = CF.solve_batch(specs, nthreads=min(sample, 16), **kwc)
+                kwc = dict(kw, max_iter=cap, riccati=True, **fk.opts_kw())
+                res = [G.solve_batch([sp_], nthreads=1, L=CF.lib(), w0=(None if w is None else w[i]), **kwc)
+                       for i, sp_ in enumerate(specs)]
+                w = np.vstack([r[0] for r in res])
+                R = [r[1][0] for r in res]
             tc = time.perf_counter() - t1
             wg = bufs[-1]["w"][:sample].cpu().numpy()
             both = np.array([r.status == 0 for r in R]) & (st[:sample] == 0)
             rec["gpu_vs_cpu"] = {"horizons": sample, "both_converged": int(both.sum()),
                                  "max_dx": (float(np.abs(_x_traj(wg[both], nx, nu, N) - _x_traj(w[both], nx, nu, N)).max())
                                             if both.any() else None),
-                                 "cpu_seconds": tc}
+                                 "cpu_seconds": tc, "cpu_one_thread_horizons_per_s": sample / tc,
+                                 "cpu_note": "the same stages on one host thread per horizon (Riccati KKT, -O3 host "
+                                             "build of the product's node functions, oracle/libmfcpu.so)"}
         out[name] = rec
         print(f"[generic_bench] {name}: {json.dumps(rec)}", file=sys.stderr, flush=True)
     return out
