@@ -317,10 +317,17 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     const MArr M{&Gm.m[0].get(), &Gm.m[FAM::NM - 1].get()};
     const FArr F{&Gm.f[0], &Gm.f[FAM::NM - 1]};
     GSTAMP_INIT;
-    __shared__ double Hs[NV * NV], Ps[NX * NX], T1[NX * NU], T2[NX * NX], Ab[NX * NX], Bb[NX * NU], Qxx[NX * NX];
+    // LDS is what limits the phase kernels' occupancy, so buffers whose lives do not overlap share storage:
+    // Rh (the stage's Q_ux / constraint rows) lives in T1 once Q_uu has consumed P B; the feedback Kf in rows
+    // NX.. of Hs once K_k and Rh have been formed from them (Q_xx stays in place in the rows < NX of Hs);
+    // the pivoted multi-column solve's scratch in A|B once the products are formed.
+    constexpr int NT1 = NX * NU > NK * NX ? NX * NU : NK * NX;
+    static_assert(NK * NX <= NU * NV, "Kf must fit in rows NX.. of Hs");
+    static_assert(NK <= 24 || NK * NX <= NX * NX + NX * NU, "the solve's scratch must fit in A|B");
+    __shared__ double Hs[NV * NV], Ps[NX * NX], T1[NT1], T2[NX * NX], AB[NX * NX + NX * NU];
+    double *const Ab = AB, *const Bb = AB + NX * NX, *const Rh = T1, *const Kf = Hs + NX * NV;
     constexpr int KSTG = NK * LDK + 2 * NK;  // per stage: factored block, perm, piv
-    constexpr int NYS = NK * (NX > 1 ? NX : 1);
-    __shared__ double Ks[NK * LDK], Ys[NYS], Rh[NK * NX], Kf[NK * NX], Jn[NEA * NX], Dds[NIA];
+    __shared__ double Ks[NK * LDK], Ys[NK], Jn[NEA * NX], Dds[NIA];  // Ys: the one-column solve's scratch
     __shared__ int perm[NK], piv[NK];
     __shared__ double vx[NV], tv[NX], zv[NK], pvs[NX], dxs[NX], dxn[NX], duv[NK];
     // stage k's record parts staged into LDS by coalesced lane-strided loads (stage_in): the inner
@@ -635,7 +642,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             }
             tile_gemm<NX, NX, NX>(
                 lane, [&](int i, int j) { return Hs[i * NV + j]; }, [&](int l, int i) { return Ab[l * NX + i]; },
-                [&](int l, int j) { return T2[l * NX + j]; }, [&](int i, int j, double v) { Qxx[i * NX + j] = v; });
+                [&](int l, int j) { return T2[l * NX + j]; }, [&](int i, int j, double v) { Hs[i * NV + j] = v; });
             __syncthreads();
             GSTAMP(11);
             // natural-order pivots in registers (the common case), the pivoted LDS factorisation otherwise
@@ -654,13 +661,13 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             __syncthreads();
             // one lane per right-hand side with the column in registers up to NK = 24 (register budget)
             if constexpr (NK <= 24) bk_solve_cols<LDK, NX, NK>(Ks, perm, piv, Kf, NX);
-            else bk_solve_wave<LDK, NX>(Ks, NK, perm, piv, Kf, NX, Ys);
+            else bk_solve_wave<LDK, NX>(Ks, NK, perm, piv, Kf, NX, AB);
             for (int e = lane; e < NK * NX; e += 64) Fg[(size_t)k * NK * NX + e] = Kf[e];
             __syncthreads();
             GSTAMP(13);
             if (k > 0) {
                 tile_gemm<NX, NX, NK>(
-                    lane, [&](int i, int j) { return Qxx[i * NX + j]; }, [&](int a, int i) { return Rh[a * NX + i]; },
+                    lane, [&](int i, int j) { return Hs[i * NV + j]; }, [&](int a, int i) { return Rh[a * NX + i]; },
                     [&](int a, int j) { return Kf[a * NX + j]; }, [&](int i, int j, double v) { T2[i * NX + j] = v; });
                 __syncthreads();
                 for (int e = lane; e < NX * NX; e += 64) Ps[e] = 0.5 * (T2[e] + T2[(e % NX) * NX + e / NX]);
