@@ -91,13 +91,16 @@ struct BKInertia {
 
 // perm/piv: LDS int arrays of length >= m.
 template <int LD>
-__device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv) {
+__device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv, int k0 = 0,
+                                                     BKInertia in0 = BKInertia{0, 0, 0}) {
+    // k0 > 0: columns 0..k0-1 were already eliminated with 1x1 pivots in natural order (bk_factor_regs<.., K0>),
+    // their inertia is in0 and perm / piv of those rows are set; the factorisation continues at column k0
     const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
-    BKInertia in{0, 0, 0};
-    for (int i = lane; i < m; i += 64) perm[i] = i;
+    BKInertia in = in0;
+    for (int i = lane + k0; i < m; i += 64) perm[i] = i;
     __syncthreads();
-    int k = 0;
+    int k = k0;
     while (k < m) {
         // pivot search: every lane scans the (<= m) candidates itself from LDS broadcast reads --
         // a serial scan of a short column is far cheaper than a 64-lane shuffle reduction
@@ -498,8 +501,11 @@ __device__ __forceinline__ void bk_solve_cols(const double *A, const int *perm, 
 // k < j <= i, the same arithmetic in the same order as bk_factor_wave, so the factor (L below
 // the diagonal, D on it; perm = identity, piv = 1) and the inertia are identical.  Returns false,
 // with A, perm and piv untouched, as soon as a pivot would need the pivoted path.
-template <int LD, int M>
-__device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, BKInertia &in) {
+// K0 < M: only columns 0..K0-1 are eliminated (the caller continues with bk_factor_wave from column K0): rows >= K0
+// are written back with their multipliers and the Schur-updated trailing block in both triangles.
+template <int LD, int M, int K0 = M>
+__device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, BKInertia &in, int *fail_col = nullptr) {
+    static_assert(K0 <= M, "K0 <= M");
     static_assert(M <= 64, "one row per lane");
     const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
@@ -509,7 +515,7 @@ __device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, B
     int pos = 0, neg = 0;
     bool ok = true;
 #pragma unroll
-    for (int k = 0; k < M; k++) {
+    for (int k = 0; k < K0; k++) {
         if (ok) {
             double r[M];
             double colmax = 0.0;
@@ -523,6 +529,7 @@ __device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, B
             const bool keep = absakk >= alpha * colmax;
             if (fmax(absakk, colmax) == 0.0 || !keep) {
                 ok = false;
+                if (fail_col) *fail_col = k;
             } else {
                 if (d > 0) pos++; else neg++;
                 const double inv = 1.0 / d;
@@ -539,10 +546,14 @@ __device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, B
     if (!ok) return false;
     if (lane < M) {
 #pragma unroll
-        for (int j = 0; j < M; j++)
+        for (int j = 0; j < M; j++) {
             if (j <= lane) A[lane * LD + j] = a[j];
-        perm[lane] = lane;
-        piv[lane] = 1;
+            if (K0 < M && j >= K0 && j < lane) A[j * LD + lane] = a[j];  // trailing block: upper mirror
+        }
+        if (lane < K0) {
+            perm[lane] = lane;
+            piv[lane] = 1;
+        }
     }
     wave_lds_sync();
     in.pos = pos;

@@ -648,7 +648,29 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             // natural-order pivots in registers (the common case), the pivoted LDS factorisation otherwise
             BKInertia in;
             // (stage blocks with at most two constraint rows: with more, the Schur rows usually need pivoting)
-            if (!(NET <= 2 && bk_factor_regs<LDK, NK>(Ks, perm, piv, in))) in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+#ifdef MF_GSTAMPS
+            // diagnostic: the register path on every family, and where it stops (slot 27: sum of the failing
+            // column, 28: failures, 29: failures in the control rows)
+            {
+                int fc = -1;
+                if (!bk_factor_regs<LDK, NK>(Ks, perm, piv, in, &fc)) {
+                    in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+                    GSTAMP_COUNT(27, fc);
+                    GSTAMP_COUNT(28, 1);
+                    GSTAMP_COUNT(29, fc < NU ? 1 : 0);
+                }
+            }
+#else
+            if constexpr (NET <= 2) {
+                if (!bk_factor_regs<LDK, NK>(Ks, perm, piv, in)) in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+            } else {
+                // many constraint rows (Centauro): the control rows in registers (they keep the natural order),
+                // the Schur rows of the constraints by the pivoted LDS routine from column NU
+                BKInertia in0;
+                if (bk_factor_regs<LDK, NK, NU>(Ks, perm, piv, in0)) in = bk_factor_wave<LDK>(Ks, NK, perm, piv, NU, in0);
+                else in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+            }
+#endif
             GSTAMP(12);
             if (in.zero) return 2;
             if (in.pos != NU || in.neg != NET) return 1;

@@ -58,3 +58,7 @@ for c, nm in zip(cols, names):
     print(f"{nm:18s} {np.median(a[:, c] / it):12.0f} cyc/iter  {100 * a[:, c].sum() / tot.sum():5.1f}%")
 print("factorisations / iter", np.mean(a[:, 20] / it), " trial merits / iter", np.mean(a[:, 21] / it),
       " SOC directions / iter", np.mean(a[:, 22] / it))
+nf = a[:, 28].sum()
+if nf > 0:
+    print("register Bunch-Kaufman failures / iter", np.mean(a[:, 28] / it), " mean failing column", a[:, 27].sum() / nf,
+          " share in the control rows", a[:, 29].sum() / nf)
