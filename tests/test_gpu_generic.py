@@ -317,3 +317,53 @@ def test_centauro_gpu_winding_bound_active():
     assert T_gpu.max() <= 80.0 + 1e-8
     _, r_cold = G.solve(cold, **kw)
     assert float(r.obj[0]) > r_cold.obj + 0.1
+
+
+def test_generic_bench_workloads_match_host_ipm():
+    """The bench's generic figures (tools/generic_bench.py, BASELINE configs 3 and 4): a few of its perturbed starts,
+    solved by the device exactly as the bench does (C3 shared budget N=100 through the capped pos_toll homotopy,
+    C4 Centauro N=50 from sol0), equal the host IPM (Riccati KKT, the same stages and caps) on every state; the
+    batched device solve of the starts equals their single solves."""
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from generic_bench import GENERIC_STAGE_CAPS, _golden_q0
+    from oracle import cpu_fast as CF
+
+    rng = np.random.default_rng(0)
+    q0b = _golden_q0()
+    sp3 = PR.box_shared_fatigue(N=100, q0=q0b)
+    X3 = np.hstack([q0b[None] + rng.uniform(-0.01, 0.01, (2, 12)), np.tile(sp3["T0"], (2, 1))])
+    stages3 = [dict(sp3, pos_toll=t) for t in PR.box_homotopy_tolerances()]
+    sp4 = PR.centauro(N=50, T=2.0)
+    q0c = np.asarray(sp4["q0"])
+    X4 = np.hstack([q0c[None] + rng.uniform(-0.02, 0.02, (3, 14)), np.tile(sp4["T0"], (3, 1))])
+    cases = [(sp3, X3, stages3, GENERIC_STAGE_CAPS, dict(u_init=PR.box_u_init(sp3), max_soc=4)),
+             (sp4, X4, [sp4], [500], dict(u_init=PR.centauro_u_init(sp4), max_soc=4))]
+    for spec, X, stages, caps, kw in cases:
+        nq = len(spec["q0"])
+        w = None
+        for st, cap in zip(stages, caps):
+            r = GOCP(st).solve(x0=X, w0=w, max_iter=cap, **kw)
+            w = r.w
+        assert (r.status == 0).all(), r.status
+        fk = CF.FastNodes(spec)
+        for i in range(X.shape[0]):
+            wc = None
+            for st, cap in zip(stages, caps):
+                sp_i = dict(st, q0=list(X[i, :nq]), T0=list(X[i, nq:]))
+                wc, R = G.solve_batch([sp_i], nthreads=1, L=CF.lib(), w0=wc, max_iter=cap, riccati=True,
+                                      **dict(kw, **fk.opts_kw()))
+                wc = wc[0]
+            assert R[0].status == 0
+            g = GOCP(stages[0])
+            nx, nu, N = g.nx, g.nu, g.N
+            xg = np.vstack([r.w[i][:nx][None], r.w[i][nx:].reshape(N, nu + nx)[:, nu:]])
+            xc = np.vstack([wc[:nx][None], wc[nx:].reshape(N, nu + nx)[:, nu:]])
+            assert np.abs(xg - xc).max() < 1e-6
+        # batched = single
+        w1 = None
+        for st, cap in zip(stages, caps):
+            r1 = GOCP(st).solve(x0=X[:1], w0=w1, max_iter=cap, **kw)
+            w1 = r1.w
+        assert np.abs(r1.w[0] - r.w[0]).max() < 1e-9
