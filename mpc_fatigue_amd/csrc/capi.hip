@@ -813,7 +813,7 @@ extern "C" int mf_node_eval(const mf_problem *pc, const double *x, const double 
     else
         return fail(MF_ERR_UNSUPPORTED, "no node-eval instantiation for this problem");
     HIPCHK(hipGetLastError());
-    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipStreamSynchronize(0));  // the launch's own (null) stream, not every stream of the device
     HIPCHK(hipMemcpy(xnext, dxn.p, sizeof(double) * n * (size_t)nodes, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(g, dg.p, sizeof(double) * (n + nl) * (size_t)nodes, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(cost, dc.p, sizeof(double) * (size_t)nodes, hipMemcpyDeviceToHost));

@@ -1622,7 +1622,7 @@ static int grec_core(mf_gproblem *p, const double *xu, const double *yi, const d
     const DevFrame *F1 = p->dF1 ? p->dF1 : p->dF0;
     hipLaunchKernelGGL(k_grec<FAM>, dim3(1), dim3(256), 0, 0, p->dM0, M1, p->dF0, F1, p->P, a.p, b2.p, c.p, d.p, l.p, o.p);
     GHIPCHK(hipGetLastError());
-    GHIPCHK(hipDeviceSynchronize());
+    GHIPCHK(hipStreamSynchronize(0));  // the launch's own (null) stream
     GHIPCHK(hipMemcpy(rec, o.p, sizeof(double) * D::REC, hipMemcpyDeviceToHost));
     return D::REC;
 }
@@ -1636,6 +1636,7 @@ template <class FAM> static int gdual_core(mf_gproblem *p, int b, double *out) {
     double *src[] = {A.lam, A.yi, A.ye, A.zxL, A.zxU, A.zuL, A.zuU, A.vL, A.vU};
     const size_t len[] = {Z.l(), Z.i(), Z.e(), Z.x(), Z.x(), Z.u(), Z.u(), Z.i(), Z.i()};
     size_t off = 0;
+    // diagnostic read of the last solve, whichever stream it ran on: the whole device is synchronised
     GHIPCHK(hipDeviceSynchronize());
     for (int a = 0; a < 9; a++) {
         GHIPCHK(hipMemcpy(out + off, src[a] + (size_t)b * len[a], len[a] * sizeof(double), hipMemcpyDeviceToHost));
