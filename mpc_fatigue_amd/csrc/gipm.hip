@@ -42,6 +42,7 @@ struct GArrays {
     double *dx, *du, *ds, *dlam, *dye, *dyi, *dzxL, *dzxU, *dzuL, *dzuU, *dvL, *dvU;
     double *bk;     // saved direction (second-order corrections)
     double *rec;    // node records
+    double *scr;    // per-node sweep scratch (FAM::Scratch images, k_geval -> k_gasm)
     double *Sx, *gx, *Su, *gu, *Ss, *gs;
     double *rdyn, *rin, *req, *trdyn, *trin, *treq, *sdyn, *sin_, *seq;
     double *tx, *tu, *ts;
@@ -98,8 +99,7 @@ __device__ __forceinline__ void gsync() {
 // instruction of the copy in flight at once; the next gsync()'s vmcnt(0) retires them).  Dword granularity:
 // the record fields are only 8-byte aligned.  The LDS destination of one instruction is the wave-uniform
 // base + 4 x lane, so lanes past the end are masked off (they would write beyond the array).
-__device__ __forceinline__ void glds_copy(double *lds, const double *src, int nd) {
-    const int lane = threadIdx.x;
+__device__ __forceinline__ void glds_copy(double *lds, const double *src, int nd, int lane = threadIdx.x) {
     const int nw = 2 * nd;
     const unsigned *s = reinterpret_cast<const unsigned *>(src);
     unsigned *d = reinterpret_cast<unsigned *>(lds);
@@ -185,16 +185,29 @@ struct FArr {
     const FArr F{&Gm.f[0], &Gm.f[FAM::NM - 1]}
 
 // ============================================================== node records
+// Two kernels per evaluation.  k_geval: lanes (problem, node, tangent direction) run the models and the
+// forward-over-reverse sweeps (FAM::prepass / seeds / lane); the per-node scratch they leave in LDS is
+// written to A.scr.  The sweeps need ~512 VGPRs (one wave per SIMD), so the record assembly, which is
+// branchy per-entry work over LDS (FAM::rec), runs in k_gasm instead: one wave per node, 64 lanes over the
+// record entries, at the occupancy its own registers allow.
+template <class FAM> constexpr int scr_words() {
+    static_assert(sizeof(typename FAM::Scratch) % sizeof(double) == 0, "scratch is a double array");
+    return (int)(sizeof(typename FAM::Scratch) / sizeof(double));
+}
+
 template <class FAM>
 __global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                                const DevFrame *F1, GParams P, GArrays A, int batch) {
     using D = typename FAM::D;
-    constexpr int L = FAM::LANES, NPB = 256 / L;
+    constexpr int L = FAM::LANES, NPB = 256 / L, SW = scr_words<FAM>();
+#ifdef MF_GSTAMPS
+    const unsigned long long gs0_ = __builtin_amdgcn_s_memtime();
+#endif
     GMODELS(FAM);
     __shared__ typename FAM::Scratch S[NPB];
     const int tid = threadIdx.x, g = tid / L, t = tid % L;
     const int N = P.N;
-    const long node = (long)blockIdx.x * NPB + g;
+    const long node0 = (long)blockIdx.x * NPB, node = node0 + g;
     bool run = g < NPB && node < (long)batch * N;
     int b = 0, k = 0;
     if (run) {
@@ -205,7 +218,7 @@ __global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevMode
     const GSz<D> Z(N);
     const double *x = A.x + b * Z.x() + (size_t)k * D::NX, *u = A.u + b * Z.u() + (size_t)k * D::NU;
     const double *yi = A.yi + b * Z.i() + (size_t)k * D::NIA, *ye = A.ye + b * Z.e() + (size_t)k * D::NET;
-    const double *lam = A.lam + b * Z.l() + (size_t)k * D::NX, *lref = A.lref + FAM::LREF * b;
+    const double *lam = A.lam + b * Z.l() + (size_t)k * D::NX;
     const bool eqon = D::NE > 0 && k >= P.eq_from && k < N;
     if (run && t < FAM::PRE) FAM::prepass(M, F, P, x, u, t, S[g]);
     __syncthreads();
@@ -213,10 +226,68 @@ __global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevMode
     __syncthreads();
     if (run) FAM::lane(M, F, x, u, yi, t, S[g]);
     __syncthreads();
-    if (run) {
-        double *rec = A.rec + b * Z.rec() + (size_t)k * D::REC;
-        for (int e = t; e < D::REC; e += L) rec[e] = FAM::rec(P, x, u, yi, ye, lam, eqon, S[g], e, lref);
+#ifdef MF_GSTAMPS
+    const unsigned long long gs1_ = __builtin_amdgcn_s_memtime();
+#endif
+    // the block's NPB scratch images are contiguous in LDS and (node-major) in A.scr
+    const long nn = (long)batch * N - node0;
+    const int nw = (int)((nn < NPB ? nn : NPB) * SW);
+    const double *src = reinterpret_cast<const double *>(S);
+    double *dst = A.scr + node0 * SW;
+    for (int e = tid; e < nw; e += 256) dst[e] = src[e];
+#ifdef MF_GSTAMPS  // slots 30 / 31: models + sweeps, scratch store (per block, charged to its first problem)
+    __syncthreads();
+    if (tid == 0 && b < 1024) {
+        atomicAdd(&mf_gstamp_buf[b * 32 + 30], gs1_ - gs0_);
+        atomicAdd(&mf_gstamp_buf[b * 32 + 31], __builtin_amdgcn_s_memtime() - gs1_);
     }
+#endif
+}
+
+template <class FAM>
+__global__ __launch_bounds__(256) void k_gasm(GParams P, GArrays A, int batch) {
+    using D = typename FAM::D;
+    constexpr int SW = scr_words<FAM>();
+    constexpr int NX = D::NX, NU = D::NU, NIA = D::NIA, NET = D::NET;
+    constexpr int VX = 0, VU = NX, VI = NX + NU, VE = VI + NIA, VL = VE + NET, NVEC = VL + NX;
+    // the scratch and the node's primal / dual values in LDS: FAM::rec reads them per entry, and from global
+    // memory every entry would wait on a load the record stores keep the compiler from hoisting
+    __shared__ typename FAM::Scratch S[4];
+    __shared__ double Vv[4][NVEC];
+    const int w = threadIdx.x / 64, lane = threadIdx.x % 64;
+    const int N = P.N;
+    const long node = (long)blockIdx.x * 4 + w;
+    bool run = node < (long)batch * N;
+    int b = 0, k = 0;
+    if (run) {
+        b = (int)(node / N);
+        k = (int)(node % N);
+        run = A.st[b].status == GS_RUNNING;
+    }
+    const GSz<D> Z(N);
+    double *V = Vv[w];
+    if (run) {
+        glds_copy(reinterpret_cast<double *>(&S[w]), A.scr + node * SW, SW, lane);
+        glds_copy(V + VX, A.x + b * Z.x() + (size_t)k * NX, NX, lane);
+        glds_copy(V + VU, A.u + b * Z.u() + (size_t)k * NU, NU, lane);
+        glds_copy(V + VI, A.yi + b * Z.i() + (size_t)k * NIA, NIA, lane);
+        if constexpr (NET > 0) glds_copy(V + VE, A.ye + b * Z.e() + (size_t)k * NET, NET, lane);
+        glds_copy(V + VL, A.lam + b * Z.l() + (size_t)k * NX, NX, lane);
+    }
+    gsync();
+#ifdef MF_GSTAMPS
+    const unsigned long long gs0_ = __builtin_amdgcn_s_memtime();
+#endif
+    if (run) {
+        const double *lref = A.lref + FAM::LREF * b;
+        const bool eqon = D::NE > 0 && k >= P.eq_from && k < N;
+        double *rec = A.rec + b * Z.rec() + (size_t)k * D::REC;
+        for (int e = lane; e < D::REC; e += 64)
+            rec[e] = FAM::rec(P, V + VX, V + VU, V + VI, V + VE, V + VL, eqon, S[w], e, lref);
+    }
+#ifdef MF_GSTAMPS  // slot 31 += record assembly (per wave, charged to its problem)
+    if (run && lane == 0 && b < 1024) atomicAdd(&mf_gstamp_buf[b * 32 + 31], __builtin_amdgcn_s_memtime() - gs0_);
+#endif
 }
 
 // ============================================================== initial point
@@ -1298,7 +1369,7 @@ template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **
              {&A.trdyn, Z.l()}, {&A.trin, Z.i()}, {&A.treq, Z.e()}, {&A.sdyn, Z.l()}, {&A.sin_, Z.i()},
              {&A.seq, Z.e()},  {&A.tx, Z.x()},   {&A.tu, Z.u()},   {&A.ts, Z.i()},   {&A.P, Z.P()},
              {&A.Kinv, Z.Kinv()}, {&A.Kfb, Z.Kfb()}, {&A.pv, Z.l()}, {&A.kv, Z.kv()}, {&A.x0, (size_t)D::NX},
-             {&A.lref, (size_t)FAM::LREF}};
+             {&A.lref, (size_t)FAM::LREF}, {&A.scr, (size_t)N * scr_words<FAM>()}};
 }
 
 static void gfree_ws(mf_gproblem *p) {
@@ -1383,11 +1454,13 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     GHIPCHK(hipGetLastError());
     constexpr int NPB = 256 / FAM::LANES;
     const int eval_blocks = (int)(((long)batch * P.N + NPB - 1) / NPB);
+    const int rec_blocks = (int)(((long)batch * P.N + 3) / 4);
     int active = batch;
     const int chunk = 4;
     for (int it = 0; it <= P.max_iter && active > 0; it += chunk) {
         for (int c = 0; c < chunk; c++) {
             hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
+            hipLaunchKernelGGL(k_gasm<FAM>, dim3(rec_blocks), dim3(256), 0, s, P, A, batch);
             hipLaunchKernelGGL(k_gpre<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             hipLaunchKernelGGL(k_gls<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);

@@ -58,6 +58,9 @@ for c, nm in zip(cols, names):
     print(f"{nm:18s} {np.median(a[:, c] / it):12.0f} cyc/iter  {100 * a[:, c].sum() / tot.sum():5.1f}%")
 print("factorisations / iter", np.mean(a[:, 20] / it), " trial merits / iter", np.mean(a[:, 21] / it),
       " SOC directions / iter", np.mean(a[:, 22] / it))
+ev = a[:, 30].sum() + a[:, 31].sum()
+print(f"k_geval block cycles / iter (sum over blocks, per problem): models+sweeps {a[:, 30].sum() / it.sum():.0f}, "
+      f"record assembly {a[:, 31].sum() / it.sum():.0f} ({100 * a[:, 31].sum() / max(ev, 1):.1f}% of k_geval)")
 nf = a[:, 28].sum()
 if nf > 0:
     print("register Bunch-Kaufman failures / iter", np.mean(a[:, 28] / it), " mean failing column", a[:, 27].sum() / nf,
