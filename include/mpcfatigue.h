@@ -230,6 +230,9 @@ typedef struct {
     int max_soc;           /* second-order corrections per iteration (IPOPT max_soc; 0 = off) */
     int verbose;
     int warm_start;        /* as mf_solver_opts.warm_start (IPOPT warm_start_init_point with w0) */
+    int filter;            /* 1: IPOPT's globalisation -- filter line search, watchdog, soft restoration and the
+                              restoration phase (elastic path rows, exact dynamics); 0: the l1-merit search */
+    double bound_relax;    /* IPOPT bound_relax_factor (1e-8 in IPOPT; 0 = exact bounds) */
 } mf_gopts;
 
 int mf_gproblem_create(const mf_model *m0, const mf_model *m1, const mf_gspec *spec, mf_gproblem **out);

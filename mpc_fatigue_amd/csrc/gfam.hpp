@@ -60,6 +60,8 @@ struct GParams {
     int force_from, tier1_from, tier1_to;  // first force control; u range regularised first (concave cost)
     int target_decimals;                   // CentauroFam: round the relative-pose targets (-1: exact)
     int dc_always;                         // delta_c from the first factorisation (rank-deficient rows)
+    int filter;                            // IPOPT's globalisation (filter, watchdog, restoration; gipm.hip)
+    int pad_f;
 };
 
 template <int NX_, int NU_, int NI_, int NE_, int NM_ = 0> struct GDims {
@@ -156,6 +158,7 @@ template <bool TH> struct BoxFamT {
     struct Scratch {
         double E[NARM][3], tau[NARM][NJ], seed[NARM][3], d[3], dF[3], eb[3];
         double cw[NARM][NJ], om[NARM][NJ];     // torque weights of the sweeps, thermal Gauss-Newton weights
+        double ow;                             // objective weight of the derivatives (0: restoration phase)
         double col[NARM][NDIR][LCOL];
     };
     // variables: q_L 0-5, q_R 6-11, (T 12-23) | qd_L, qd_R (NX..NX+11), F_L, F_R (NX+12..NX+17)
@@ -220,14 +223,15 @@ template <bool TH> struct BoxFamT {
     //   g = w_box |(E1+E2)/2 - p|^2 + ye (|d|^2 - L) + y_m . (d x dF),  d = E1 - E2, dF = F_L - F_R
     // and the torque weights c = y_tau (+ 2 tau lam_T b Ra / ktau^2 with the thermal state)
     MF_HD static void seeds(const GParams &P, const double *u, const double *yi, const double *ye, const double *lam,
-                            bool eqon, Scratch &S) {
+                            bool eqon, double ow, Scratch &S) {
         const double yev = eqon ? ye[0] : 0.0;
         const double *ym = yi + 3;
         double dFxy[3];
+        S.ow = ow;
         for (int r = 0; r < 3; r++) {
             S.d[r] = S.E[0][r] - S.E[1][r];
             S.dF[r] = u[12 + r] - u[15 + r];
-            S.eb[r] = P.w_box * (0.5 * (S.E[0][r] + S.E[1][r]) - P.box_pdes[r]);
+            S.eb[r] = ow * P.w_box * (0.5 * (S.E[0][r] + S.E[1][r]) - P.box_pdes[r]);
         }
         cross3(dFxy, S.dF, ym);
         for (int r = 0; r < 3; r++) {
@@ -275,7 +279,7 @@ template <bool TH> struct BoxFamT {
         var(c, kc, ac, lc);
         using L = GLaneOut<NJ>;
         double w = 0.0;
-        if (kr == 3 || kc == 3) return (r == c) ? 2.0 * P.wT : 0.0;  // T enters linearly (plus wT |T|^2)
+        if (kr == 3 || kc == 3) return (r == c) ? 2.0 * S.ow * P.wT : 0.0;  // T enters linearly (plus wT |T|^2)
         // arm sweeps (phi_a = c.tau_a + seed_a . E_a)
         if (ar == ac && !(kr == 2 && kc == 2)) {
             auto colent = [&](int vdir, int kind, int loc) {  // column vdir of arm ar, row (kind, loc)
@@ -297,7 +301,7 @@ template <bool TH> struct BoxFamT {
         // algebraic part: J_E^T (d^2 g / dE dE) J_E and the E-F cross terms of the moment rows
         const double yev = eqon ? ye[0] : 0.0;
         if (kr == 0 && kc == 0) {
-            const double g = 0.5 * P.w_box + (ar == ac ? 2.0 : -2.0) * yev;
+            const double g = 0.5 * S.ow * P.w_box + (ar == ac ? 2.0 : -2.0) * yev;
             double acc = 0.0;
             for (int k = 0; k < 3; k++) acc += JE(S, ar, k, r) * JE(S, ac, k, c);
             w += g * acc;
@@ -309,7 +313,7 @@ template <bool TH> struct BoxFamT {
             w += sgn * acc;
         }
         if (r == c && kr == 1) {
-            w += 2.0 * P.w_qdb;
+            w += 2.0 * S.ow * P.w_qdb;
             if constexpr (TH) w += lam[NQ + NJ * ar + lr] * P.th_b * 2.0 / P.Rh;
         }
         return w;
@@ -342,8 +346,8 @@ template <bool TH> struct BoxFamT {
                 for (int c = 0; c < 3; c++) acc += JE(S, a, c, v) * S.eb[c];
                 return acc;
             }
-            if (k == 3) return 2.0 * P.wT * x[v];
-            return k == 1 ? 2.0 * P.w_qdb * u[v - NX] : 0.0;
+            if (k == 3) return 2.0 * S.ow * P.wT * x[v];
+            return k == 1 ? 2.0 * S.ow * P.w_qdb * u[v - NX] : 0.0;
         }
         if (e < D::O_JI) {  // c_in values
             const int r = e - D::O_CI;
@@ -425,6 +429,7 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
     static constexpr int LCOL = GLaneOut<NJ>::LCOL;
     struct Scratch {
         double E[1][3], tau[1][NJ], pf[3], cw[NJ], om[NJ], seed[3], Fw[3];
+        double ow;  // objective weight of the derivatives (0: restoration phase)
         double col[1][NDIR][LCOL];
     };
     // variables: q 0..NJ-1, (T NJ..2NJ-1) | qd, F
@@ -476,9 +481,10 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
     // torque weights c_j = yi_j + 2 tau_j (wtau + lam_T,j b Ra / ktau_j^2), Gauss-Newton weights
     // om_j = 2 (wtau + lam_T,j b Ra / ktau_j^2), frame seed = (ye, 0)
     MF_HD static void seeds(const GParams &P, const double *, const double *yi, const double *ye, const double *lam,
-                            bool eqon, Scratch &S) {
+                            bool eqon, double ow, Scratch &S) {
+        S.ow = ow;
         for (int j = 0; j < NJ; j++) {
-            double w = P.wtau;
+            double w = ow * P.wtau;
             if constexpr (TH) w += lam[NJ + j] * P.th_b * P.Ra / (P.ktau[j] * P.ktau[j]);
             S.om[j] = 2.0 * w;
             S.cw[j] = yi[j] + 2.0 * w * S.tau[0][j];
@@ -528,11 +534,11 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
         }
         if (r == c) {
             if (kr == 1) {
-                w += 2.0 * P.wqd;
+                w += 2.0 * S.ow * P.wqd;
                 if constexpr (TH) w += lam[NJ + lr] * P.th_b * 2.0 / P.Rh;
             }
-            if (kr == 2) w += 2.0 * P.wF;
-            if (kr == 3) w += 2.0 * P.wT;
+            if (kr == 2) w += 2.0 * S.ow * P.wF;
+            if (kr == 3) w += 2.0 * S.ow * P.wT;
         }
         return w;
     }
@@ -561,7 +567,7 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
             if (k == 1) g += 2.0 * P.wqd * u[l];
             if (k == 2) g += 2.0 * P.wF * u[NJ + l];
             if (k == 3) g += 2.0 * P.wT * x[NJ + l];
-            return g;
+            return S.ow * g;
         }
         if (e < D::O_JI) return S.tau[0][e - D::O_CI];
         if (e < D::O_CE) {
@@ -636,6 +642,7 @@ struct CentauroFam {
         double tau[NARM][NJ], c[NARM][NJ], om[NARM][NJ];
         ArmPose<NJ> P[NARM];
         double eb[3], dF[3], yr[3], yo[3], ym[3];
+        double ow;  // objective weight of the derivatives (0: restoration phase)
         double col[NARM][NDIR][LCOL];
     };
     // variables: q 0..13 (arm v / 7), T 14..27 | qd 28..41, F_L 42..44, F_R 45..47
@@ -719,7 +726,8 @@ struct CentauroFam {
     // torque weights c = yi + 2 tau lam_T b Ra / ktau^2 (the arm sweeps), Gauss-Newton weights om, and the
     // multipliers of the pose functions (closed form)
     MF_HD static void seeds(const GParams &P, const double *u, const double *yi, const double *ye, const double *lam,
-                            bool eqon, Scratch &S) {
+                            bool eqon, double ow, Scratch &S) {
+        S.ow = ow;
         for (int a = 0; a < NARM; a++)
             for (int j = 0; j < NJ; j++) {
                 const int i = NJ * a + j;
@@ -728,7 +736,7 @@ struct CentauroFam {
                 S.c[a][j] = yi[i] + 2.0 * w * S.tau[a][j];
             }
         for (int r = 0; r < 3; r++) {
-            S.eb[r] = P.w_box * (0.5 * (S.P[0].p[r] + S.P[1].p[r]) - P.box_pdes[r]);
+            S.eb[r] = ow * P.w_box * (0.5 * (S.P[0].p[r] + S.P[1].p[r]) - P.box_pdes[r]);
             S.dF[r] = u[NQ + r] - u[NQ + 3 + r];
             S.yr[r] = eqon ? ye[r] : 0.0;
             S.yo[r] = eqon ? ye[3 + r] : 0.0;
@@ -821,7 +829,7 @@ struct CentauroFam {
     MF_HD static double D2(const GParams &P, const Scratch &S, const PV &V, const PV &W) {
         const ArmPose<NJ> &L = S.P[0], &Rr = S.P[1];
         double acc = 0.0;
-        for (int k = 0; k < 3; k++) acc += 0.5 * P.w_box * (V.dp[0][k] + V.dp[1][k]) * (W.dp[0][k] + W.dp[1][k]);
+        for (int k = 0; k < 3; k++) acc += 0.5 * S.ow * P.w_box * (V.dp[0][k] + V.dp[1][k]) * (W.dp[0][k] + W.dp[1][k]);
         for (int b = 0; b < 3; b++) {
             double t = 0.0;
             for (int k = 0; k < 3; k++)
@@ -894,9 +902,9 @@ struct CentauroFam {
             w += S.ym[0] * m[0] + S.ym[1] * m[1] + S.ym[2] * m[2];
         }
         if (r == c) {
-            if (kr == 2) w += 2.0 * P.w_qdb + lam[NQ + NJ * ar + lr] * P.th_b * 2.0 / P.Rh;
-            if (kr == 3) w += 2.0 * P.wF;
-            if (kr == 1) w += 2.0 * P.wT;
+            if (kr == 2) w += 2.0 * S.ow * P.w_qdb + lam[NQ + NJ * ar + lr] * P.th_b * 2.0 / P.Rh;
+            if (kr == 3) w += 2.0 * S.ow * P.wF;
+            if (kr == 1) w += 2.0 * S.ow * P.wT;
         }
         return w;
     }
@@ -926,9 +934,9 @@ struct CentauroFam {
                 var1(S, a, l, V);
                 return D1(S, S.eb, z3, z3, z3, V);
             }
-            if (k == 1) return 2.0 * P.wT * x[v];
-            if (k == 2) return 2.0 * P.w_qdb * u[v - D::NX];
-            return 2.0 * P.wF * u[v - D::NX];
+            if (k == 1) return 2.0 * S.ow * P.wT * x[v];
+            if (k == 2) return 2.0 * S.ow * P.w_qdb * u[v - D::NX];
+            return 2.0 * S.ow * P.wF * u[v - D::NX];
         }
         if (e < D::O_JI) {
             const int r = e - D::O_CI;

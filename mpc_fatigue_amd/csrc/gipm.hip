@@ -34,8 +34,28 @@ struct GState {
     double mu, nu, reg_last, E0, cviol, obj;
     double dw_c, dc_c;  // the regularisation the accepted factorisation was made with (k_gkkt -> k_gls)
     int reg_tier, status, iter, n_ls_fail, n_ic, consec_fail, n_soc, pad;
+    // IPOPT mode (GParams::filter; the same algorithm as oracle/mf_ocp.c mfg_opts.filter with resto_hard_dyn)
+    double ic_last, ic_last_main;  // last nonzero inertia perturbation: current problem / main problem in a restoration
+    double thm[2][2];              // theta_max / theta_min of the main / restoration filter (< 0: unset)
+    double rs_ph, rs_th;           // main problem's line-search reference where the restoration started
+    double mu_orig, zeta;          // main problem's mu during a restoration; proximity weight sqrt(mu_resto)
+    double wd_ph, wd_th, wd_gd, wd_atest;  // watchdog reference
+    double pd_cur;                 // soft restoration: primal-dual error before the pending step
+    int mode;                      // 0 main problem, 1 restoration problem
+    int pend;                      // GP_*: pending action of the next phases
+    int nf[2];                     // filter entries (main, restoration)
+    int in_wd, wd_short, wd_trial, in_soft, soft_cnt, n_resto, n_wd, n_soft;
 };
-enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INERTIA = 3 };
+enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INERTIA = 3, GS_RESTOFAIL = 4,
+       GS_LOCINF = 5 };
+// pending actions (IPOPT mode):
+//   GP_SOFT        the last k_gls took a soft-restoration step: k_gpre compares the primal-dual errors
+//   GP_RESTO       k_gpre sets up the restoration problem at the current point (records current)
+//   GP_LSM         k_gkkt / k_gls compute the restoration problem's least-square multipliers
+//   GP_IDLE(_RESTO) the records are stale (a restoration ended / a soft step was undone): k_gkkt and k_gls idle,
+//                  the next iteration re-evaluates (and then sets up the restoration)
+enum { GP_NONE = 0, GP_SOFT = 1, GP_RESTO = 2, GP_LSM = 3, GP_IDLE = 4, GP_IDLE_RESTO = 5 };
+constexpr int GFCAP = 512;  // filter entries per filter (dominated entries are dropped as IPOPT does)
 
 struct GArrays {
     double *x, *u, *s, *lam, *ye, *yi, *zxL, *zxU, *zuL, *zuU, *vL, *vU;
@@ -52,6 +72,12 @@ struct GArrays {
     const double *u0, *w0;                    // optional per-problem fixed u_0 values / warm start
     GState *st;
     int *active;
+    // IPOPT mode: filters (2 x GFCAP x (phi, theta)), watchdog / soft-restoration copies of the iterate and of
+    // the direction, and the restoration problem's elastic variables p, n >= 0 on the slack rows and the
+    // equality rows (rows [k NIA + q | N NIA + k NET + e]), with their bound multipliers, steps, trial values,
+    // condensed Sigma / barrier gradients / residual corrections, and the reference point w_R, D_R^2
+    double *fil, *wdit, *wddir;
+    double *pr, *nr, *zp, *zn, *dpr, *dnr, *dzp, *dzn, *tpr, *tnr, *Sp, *Sn, *gp, *gn, *rowr, *wR, *dR;
 };
 
 template <class D> struct GSz {
@@ -64,7 +90,9 @@ template <class D> struct GSz {
     __host__ __device__ size_t e() const { return N * NE; }
     __host__ __device__ size_t l() const { return N * NX; }
     __host__ __device__ size_t rec() const { return N * D::REC; }
-    __host__ __device__ size_t bk() const { return 3 * x() + 3 * u() + 4 * i() + l() + e(); }
+    __host__ __device__ size_t nr() const { return N * (NI + NE); }  // elastic rows (restoration)
+    __host__ __device__ size_t bk() const { return 3 * x() + 3 * u() + 4 * i() + l() + e() + 4 * nr(); }
+    __host__ __device__ size_t wv() const { return x() + u(); }
     __host__ __device__ size_t P() const { return N * NX * NX; }
     __host__ __device__ size_t Kinv() const { return N * (NK * (NK + 1) + 2 * NK); }  // BK factor + perm/piv
     __host__ __device__ size_t Kfb() const { return N * NK * NX; }
@@ -139,7 +167,7 @@ __device__ unsigned long long mf_gstamp_buf[32 * 1024];
 template <int NJ> struct GModelLds {
     static constexpr int WORDS = (int)((offsetof(DevModel, j) + NJ * sizeof(DevJoint) + sizeof(double) - 1) / sizeof(double));
     double w[WORDS];
-    __device__ void load(const DevModel *g) {
+    __device__ __forceinline__ void load(const DevModel *g) {
         const double *s = reinterpret_cast<const double *>(g);
         for (int i = threadIdx.x; i < WORDS; i += blockDim.x) w[i] = s[i];
     }
@@ -149,7 +177,7 @@ template <int NJ> struct GModelLds {
 template <class FAM> struct GModels {
     GModelLds<FAM::NJ> m[FAM::NM];
     DevFrame f[FAM::NM];
-    __device__ void load(const DevModel *M0, const DevModel *M1, const DevFrame *F0, const DevFrame *F1) {
+    __device__ __forceinline__ void load(const DevModel *M0, const DevModel *M1, const DevFrame *F0, const DevFrame *F1) {
         m[0].load(M0);
         if (FAM::NM > 1) m[FAM::NM - 1].load(M1);
         const double *s0 = reinterpret_cast<const double *>(F0);
@@ -215,6 +243,7 @@ __global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevMode
         k = (int)(node % N);
         run = A.st[b].status == GS_RUNNING;
     }
+    const double ow = (run && A.st[b].mode == 1) ? 0.0 : 1.0;  // the restoration problem has no objective
     const GSz<D> Z(N);
     const double *x = A.x + b * Z.x() + (size_t)k * D::NX, *u = A.u + b * Z.u() + (size_t)k * D::NU;
     const double *yi = A.yi + b * Z.i() + (size_t)k * D::NIA, *ye = A.ye + b * Z.e() + (size_t)k * D::NET;
@@ -222,7 +251,7 @@ __global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevMode
     const bool eqon = D::NE > 0 && k >= P.eq_from && k < N;
     if (run && t < FAM::PRE) FAM::prepass(M, F, P, x, u, t, S[g]);
     __syncthreads();
-    if (run && t == 0) FAM::seeds(P, u, yi, ye, lam, eqon, S[g]);
+    if (run && t == 0) FAM::seeds(P, u, yi, ye, lam, eqon, ow, S[g]);
     __syncthreads();
     if (run) FAM::lane(M, F, x, u, yi, t, S[g]);
     __syncthreads();
@@ -358,6 +387,12 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         st.mu = P.mu_init; st.nu = 0.0; st.reg_last = 0.0; st.E0 = INFINITY; st.cviol = INFINITY; st.obj = 0.0;
         st.reg_tier = 0; st.status = GS_RUNNING; st.iter = 0; st.n_ls_fail = 0; st.n_ic = 0; st.consec_fail = 0;
         st.n_soc = 0; st.pad = 0; st.dw_c = 0.0; st.dc_c = 0.0;
+        st.ic_last = st.ic_last_main = 0.0;
+        st.thm[0][0] = st.thm[0][1] = st.thm[1][0] = st.thm[1][1] = -1.0;
+        st.rs_ph = st.rs_th = st.mu_orig = st.zeta = 0.0;
+        st.wd_ph = st.wd_th = st.wd_gd = st.wd_atest = st.pd_cur = 0.0;
+        st.mode = 0; st.pend = GP_NONE; st.nf[0] = st.nf[1] = 0;
+        st.in_wd = st.wd_short = st.wd_trial = st.in_soft = st.soft_cnt = st.n_resto = st.n_wd = st.n_soft = 0;
         A.st[b] = st;
     }
 }
@@ -369,7 +404,7 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
 //   PH 2 k_gls   fraction to the boundary, l1-merit line search with second-order corrections, update
 // The phases share this one body (same arithmetic as a single kernel); each launch keeps only its own
 // phase's code and LDS, so register allocation and occupancy are per phase.
-template <class FAM, int PH>
+template <class FAM, int PH, bool FLT>
 __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                             const DevFrame *F1, const GParams &P, const GArrays &A, int batch) {
     using D = typename FAM::D;
@@ -385,8 +420,17 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         Gm.load(M0, M1, F0, F1);
         __syncthreads();
     }
-    const MArr M{&Gm.m[0].get(), &Gm.m[FAM::NM - 1].get()};
-    const FArr F{&Gm.f[0], &Gm.f[FAM::NM - 1]};
+    // the LDS images' generic addresses made opaque: with many inlined users the optimiser otherwise folds the
+    // {&Gm.m[0], &Gm.m[1]} aggregate into a constant global initialiser, which cannot hold LDS addresses
+    const DevModel *gm0_ = nullptr, *gm1_ = nullptr;
+    const DevFrame *gf0_ = nullptr, *gf1_ = nullptr;
+    if constexpr (PH == 2) {  // (the other phases evaluate no node function: no model images in their LDS)
+        gm0_ = &Gm.m[0].get(); gm1_ = &Gm.m[FAM::NM - 1].get();
+        gf0_ = &Gm.f[0]; gf1_ = &Gm.f[FAM::NM - 1];
+        __asm__ volatile("" : "+s"(gm0_), "+s"(gm1_), "+s"(gf0_), "+s"(gf1_));
+    }
+    const MArr M{gm0_, gm1_};
+    const FArr F{gf0_, gf1_};
     GSTAMP_INIT;
     // LDS is what limits the phase kernels' occupancy, so buffers whose lives do not overlap share storage:
     // Rh (the stage's Q_ux / constraint rows) lives in T1 once Q_uu has consumed P B; the feedback Kf in rows
@@ -436,15 +480,15 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     double *kvg = A.kv + b * Z.kv();
     const double *ulo = A.u_lo, *uhi = A.u_hi, *clo = A.c_lo, *chi = A.c_hi;
     const double *lref = A.lref + FAM::LREF * b;
-    auto R = [&](int k) { return rec + (size_t)k * D::REC; };
-    auto ufix = [&](int i) { return gb(ulo[i]) && ulo[i] == uhi[i]; };
-    auto cact = [&](int k, int q) { return gb(clo[k * NI + q]) || gb(chi[k * NI + q]); };
-    auto eqon = [&](int k) { return NE > 0 && k >= P.eq_from && k < N; };
+    auto R = [&](int k) __attribute__((always_inline)) { return rec + (size_t)k * D::REC; };
+    auto ufix = [&](int i) __attribute__((always_inline)) { return gb(ulo[i]) && ulo[i] == uhi[i]; };
+    auto cact = [&](int k, int q) __attribute__((always_inline)) { return gb(clo[k * NI + q]) || gb(chi[k * NI + q]); };
+    auto eqon = [&](int k) __attribute__((always_inline)) { return NE > 0 && k >= P.eq_from && k < N; };
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99, s_max = 100.0;
     const double kappa_sigma = 1e10, eta = 1e-4, rho = 0.1;
     double mu = st.mu, nu = st.nu;
 
-    auto finish = [&](int status) {
+    auto finish = [&](int status) __attribute__((always_inline)) {
         GSTAMP_FLUSH;
         double f = 0.0;
         for (int k = lane; k < N; k += 64) f += R(k)[D::O_L];
@@ -459,120 +503,393 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         }
     };
 
-    if constexpr (PH == 0) {
-    // ---------------- optimality error (IPOPT E_0, s_max scaling)
-    double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sm = 0, sbm = 0;
-    int nm = 0, nbm = 0;
-    auto comp = [&](double z, double gap) {
-        const double c = z * gap;
-        cinf0 = fmax(cinf0, fabs(c));
-        cinfm = fmax(cinfm, fabs(c - mu));
-        sbm += z;
-        nbm++;
+    // ---------------- IPOPT mode (P.filter): restoration-phase arrays and row helpers
+    // k_gpre / k_gkkt test the option at run time; k_gls is instantiated twice (merit / filter) so that each
+    // line search has its own register allocation
+    const bool flt = PH == 2 ? FLT : P.filter != 0;
+    const bool rsm = flt && st.mode == 1;  // the restoration problem is being solved
+    constexpr double RHO_R = 1000.0, KAPPA_D = 1e-5;
+    const size_t NRo = (size_t)N * NIA;   // elastic rows: slack rows [k NIA + q], then equality rows [NRo + k NET + e]
+    double *prr = A.pr + b * Z.nr(), *nrr = A.nr + b * Z.nr(), *zpr = A.zp + b * Z.nr(), *znr = A.zn + b * Z.nr();
+    double *dpr = A.dpr + b * Z.nr(), *dnr = A.dnr + b * Z.nr(), *dzp = A.dzp + b * Z.nr(), *dzn = A.dzn + b * Z.nr();
+    double *tpr = A.tpr + b * Z.nr(), *tnr = A.tnr + b * Z.nr(), *Spr = A.Sp + b * Z.nr(), *Snr = A.Sn + b * Z.nr();
+    double *gpr = A.gp + b * Z.nr(), *gnr = A.gn + b * Z.nr(), *rowr = A.rowr + b * Z.nr();
+    double *wR = A.wR + b * Z.wv(), *dR = A.dR + b * Z.wv();
+    auto el_on = [&](int r) __attribute__((always_inline)) -> bool {  // elastic row r active
+        if ((size_t)r < NRo) return (r % NIA) < NI && cact(r / NIA, r % NIA);
+        const int e = r - (int)NRo, k = e / NET, ee = e % NET;
+        return ee < NEA ? (ee < NE && eqon(k)) : true;
     };
-    for (int e = lane; e < N * NX; e += 64) {  // x rows, k = 1..N
-        const int k = e / NX + 1, j = e % NX, i = k * NX + j;
-        double r = -lam[(k - 1) * NX + j];
-        if (k < N) {
+    auto el_y = [&](int r) __attribute__((always_inline)) -> double { return (size_t)r < NRo ? yi[r] : ye[r - NRo]; };
+    const int NRI = (int)Z.nr();
+
+    // ---------------- optimality measures at the current point (records current): IPOPT's E_0 pieces and, for
+    // the soft restoration phase, the primal-dual system error (sum of 1-norms / number of terms); the
+    // restoration problem's when rsm
+    struct GErr { double dinf, pinf, cinf0, cinfm, sd, sc, s1, n1; };
+    auto opt_err = [&](double mu_) __attribute__((always_inline)) -> GErr {
+        double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sm = 0, sbm = 0, s1 = 0;
+        int nm = 0, nbm = 0, n1 = 0;
+        auto comp = [&](double z, double gap) __attribute__((always_inline)) {
+            const double c = z * gap;
+            cinf0 = fmax(cinf0, fabs(c));
+            cinfm = fmax(cinfm, fabs(c - mu_));
+            sbm += z;
+            nbm++;
+            s1 += fabs(c - mu_);
+            n1++;
+        };
+        for (int e = lane; e < N * NX; e += 64) {  // x rows, k = 1..N
+            const int k = e / NX + 1, j = e % NX, i = k * NX + j;
+            double r = -lam[(k - 1) * NX + j];
+            if (k < N) {
+                const double *rk = R(k);
+                r += rk[D::O_GL + j];
+                for (int jj = 0; jj < NX; jj++) r += rk[D::O_A + jj * NX + j] * lam[k * NX + jj];
+                for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + j] * yi[k * NIA + q];
+                if (eqon(k))
+                    for (int ee = 0; ee < NE; ee++) r += rk[D::O_JE + ee * NX + j] * ye[k * NET + ee];
+                for (int m = 0; m < NM; m++) r += rk[D::O_JM + m * NV + j] * ye[k * NET + NEA + m];
+            }
+            if (rsm) r += st.zeta * dR[i] * (x[i] - wR[i]);
+            r += -zxL[i] + zxU[i];
+            dinf = fmax(dinf, fabs(r));
+            s1 += fabs(r);
+            n1++;
+            if (gb(P.x_lo[j])) comp(zxL[i], x[i] - P.x_lo[j]);
+            if (gb(P.x_hi[j])) comp(zxU[i], P.x_hi[j] - x[i]);
+        }
+        for (int e = lane; e < N * NU; e += 64) {  // u rows (free)
+            if (ufix(e)) continue;
+            const int k = e / NU, j = e % NU;
             const double *rk = R(k);
-            r += rk[D::O_GL + j];
-            for (int jj = 0; jj < NX; jj++) r += rk[D::O_A + jj * NX + j] * lam[k * NX + jj];
-            for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + j] * yi[k * NIA + q];
+            double r = rk[D::O_GL + NX + j];
+            for (int jj = 0; jj < NX; jj++) r += rk[D::O_B + jj * NU + j] * lam[k * NX + jj];
+            for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + NX + j] * yi[k * NIA + q];
+            for (int m = 0; m < NM; m++) r += rk[D::O_JM + m * NV + NX + j] * ye[k * NET + NEA + m];
+            if (rsm) r += st.zeta * dR[Z.x() + e] * (u[e] - wR[Z.x() + e]);
+            r += -zuL[e] + zuU[e];
+            dinf = fmax(dinf, fabs(r));
+            s1 += fabs(r);
+            n1++;
+            if (gb(ulo[e])) comp(zuL[e], u[e] - ulo[e]);
+            if (gb(uhi[e])) comp(zuU[e], uhi[e] - u[e]);
+        }
+        for (int e = lane; e < N * NI; e += 64) {  // slack rows
+            const int k = e / NI, q = e % NI, i = k * NIA + q;
+            if (!cact(k, q)) continue;
+            const double rd = -yi[i] - vL[i] + vU[i];
+            dinf = fmax(dinf, fabs(rd));
+            s1 += fabs(rd);
+            n1++;
+            if (gb(clo[e])) comp(vL[i], s[i] - clo[e]);
+            if (gb(chi[e])) comp(vU[i], chi[e] - s[i]);
+            const double rp = R(k)[D::O_CI + q] - s[i] + (rsm ? nrr[i] - prr[i] : 0.0);
+            pinf = fmax(pinf, fabs(rp));
+            s1 += fabs(rp);
+            n1++;
+            sm += fabs(yi[i]);
+            nm++;
+        }
+        for (int e = lane; e < N * NX; e += 64) {  // dynamics
+            const int k = e / NX, j = e % NX;
+            const double rp = R(k)[D::O_F + j] - x[(k + 1) * NX + j];
+            pinf = fmax(pinf, fabs(rp));
+            s1 += fabs(rp);
+            n1++;
+            sm += fabs(lam[e]);
+            nm++;
+        }
+        if (NE > 0)
+            for (int e = lane; e < N * NE; e += 64) {
+                const int k = e / NE, ee = e % NE;
+                if (!eqon(k)) continue;
+                const size_t r = NRo + (size_t)k * NET + ee;
+                const double rp = R(k)[D::O_CE + ee] + (rsm ? nrr[r] - prr[r] : 0.0);
+                pinf = fmax(pinf, fabs(rp));
+                s1 += fabs(rp);
+                n1++;
+                sm += fabs(ye[k * NET + ee]);
+                nm++;
+            }
+        if (NM > 0)
+            for (int e = lane; e < N * NM; e += 64) {
+                const int k = e / NM, m = e % NM;
+                const size_t r = NRo + (size_t)k * NET + NEA + m;
+                const double rp = R(k)[D::O_CM + m] + (rsm ? nrr[r] - prr[r] : 0.0);
+                pinf = fmax(pinf, fabs(rp));
+                s1 += fabs(rp);
+                n1++;
+                sm += fabs(ye[k * NET + NEA + m]);
+                nm++;
+            }
+        if (rsm)  // elastic variables: rho - y - z_p, rho + y - z_n, complementarity
+            for (int r = lane; r < NRI; r += 64) {
+                if (!el_on(r)) continue;
+                const double y = el_y(r), a1 = RHO_R - y - zpr[r], a2 = RHO_R + y - znr[r];
+                dinf = fmax(dinf, fmax(fabs(a1), fabs(a2)));
+                s1 += fabs(a1) + fabs(a2);
+                n1 += 2;
+                comp(zpr[r], prr[r]);
+                comp(znr[r], nrr[r]);
+            }
+        dinf = wave_max(dinf); pinf = wave_max(pinf); cinf0 = wave_max(cinf0); cinfm = wave_max(cinfm);
+        sm = wave_sum(sm); sbm = wave_sum(sbm); nm = wave_sum_i(nm); nbm = wave_sum_i(nbm);
+        s1 = wave_sum(s1); n1 = wave_sum_i(n1);
+        GErr E;
+        E.dinf = dinf; E.pinf = pinf; E.cinf0 = cinf0; E.cinfm = cinfm;
+        E.sd = fmax(s_max, (sm + sbm) / fmax(1.0, (double)(nm + nbm))) / s_max;
+        E.sc = fmax(s_max, sbm / fmax(1.0, (double)nbm)) / s_max;
+        E.s1 = s1; E.n1 = (double)n1;
+        return E;
+    };
+
+    // the filter of problem m (0 main, 1 restoration): acceptability and IPOPT's AddEntry
+    double *filb = A.fil + (size_t)b * 4 * GFCAP;
+    auto fil_ok = [&](int m, double ph, double th) __attribute__((always_inline)) -> bool {
+        const double *f = filb + 2 * m * GFCAP;
+        int bad = 0;
+        for (int j = lane; j < st.nf[m]; j += 64)
+            if (!(ph <= f[2 * j] || th <= f[2 * j + 1])) bad = 1;
+        return wave_sum_i(bad) == 0;
+    };
+    auto fil_add = [&](int m, double ph, double th) __attribute__((always_inline)) {
+        double *f = filb + 2 * m * GFCAP;
+        int n = 0;
+        if (lane == 0) {
+            for (int j = 0; j < st.nf[m]; j++)
+                if (!(ph <= f[2 * j] && th <= f[2 * j + 1])) { f[2 * n] = f[2 * j]; f[2 * n + 1] = f[2 * j + 1]; n++; }
+            if (n == GFCAP) {  // full: the oldest entry goes (not reached on the reference problems)
+                for (int j = 1; j < n; j++) { f[2 * j - 2] = f[2 * j]; f[2 * j - 1] = f[2 * j + 1]; }
+                n--;
+            }
+            f[2 * n] = ph;
+            f[2 * n + 1] = th;
+            n++;
+        }
+        st.nf[m] = __shfl(n, 0, 64);
+        gsync();
+    };
+    // barrier objective and l1 violation of the main problem at the current point (records), with mu_o
+    auto orig_merit_cur = [&](double mu_o, double &phi, double &th, bool &okp) __attribute__((always_inline)) {
+        double fs = 0.0, t = 0.0, bar = 0.0, lin = 0.0;
+        int bad = 0;
+        for (int k = lane; k < N; k += 64) {
+            const double *rk = R(k);
+            fs += rk[D::O_L];
+            for (int j = 0; j < NX; j++) t += fabs(rk[D::O_F + j] - x[(k + 1) * NX + j]);
+            for (int q = 0; q < NI; q++)
+                if (cact(k, q)) t += fabs(rk[D::O_CI + q] - s[k * NIA + q]);
             if (eqon(k))
-                for (int ee = 0; ee < NE; ee++) r += rk[D::O_JE + ee * NX + j] * ye[k * NET + ee];
-            for (int m = 0; m < NM; m++) r += rk[D::O_JM + m * NV + j] * ye[k * NET + NEA + m];
+                for (int ee = 0; ee < NE; ee++) t += fabs(rk[D::O_CE + ee]);
+            for (int m = 0; m < NM; m++) t += fabs(rk[D::O_CM + m]);
         }
-        r += -zxL[i] + zxU[i];
-        dinf = fmax(dinf, fabs(r));
-        if (gb(P.x_lo[j])) comp(zxL[i], x[i] - P.x_lo[j]);
-        if (gb(P.x_hi[j])) comp(zxU[i], P.x_hi[j] - x[i]);
-    }
-    for (int e = lane; e < N * NU; e += 64) {  // u rows (free)
-        if (ufix(e)) continue;
-        const int k = e / NU, j = e % NU;
-        const double *rk = R(k);
-        double r = rk[D::O_GL + NX + j];
-        for (int jj = 0; jj < NX; jj++) r += rk[D::O_B + jj * NU + j] * lam[k * NX + jj];
-        for (int q = 0; q < NI; q++) r += rk[D::O_JI + q * NV + NX + j] * yi[k * NIA + q];
-        for (int m = 0; m < NM; m++) r += rk[D::O_JM + m * NV + NX + j] * ye[k * NET + NEA + m];
-        r += -zuL[e] + zuU[e];
-        dinf = fmax(dinf, fabs(r));
-        if (gb(ulo[e])) comp(zuL[e], u[e] - ulo[e]);
-        if (gb(uhi[e])) comp(zuU[e], uhi[e] - u[e]);
-    }
-    for (int e = lane; e < N * NI; e += 64) {  // slack rows
-        const int k = e / NI, q = e % NI, i = k * NIA + q;
-        if (!cact(k, q)) continue;
-        dinf = fmax(dinf, fabs(-yi[i] - vL[i] + vU[i]));
-        if (gb(clo[e])) comp(vL[i], s[i] - clo[e]);
-        if (gb(chi[e])) comp(vU[i], chi[e] - s[i]);
-        pinf = fmax(pinf, fabs(R(k)[D::O_CI + q] - s[i]));
-        sm += fabs(yi[i]);
-        nm++;
-    }
-    for (int e = lane; e < N * NX; e += 64) {  // dynamics
-        const int k = e / NX, j = e % NX;
-        pinf = fmax(pinf, fabs(R(k)[D::O_F + j] - x[(k + 1) * NX + j]));
-        sm += fabs(lam[e]);
-        nm++;
-    }
-    if (NE > 0)
-        for (int e = lane; e < N * NE; e += 64) {
-            const int k = e / NE, ee = e % NE;
-            if (!eqon(k)) continue;
-            pinf = fmax(pinf, fabs(R(k)[D::O_CE + ee]));
-            sm += fabs(ye[k * NET + ee]);
-            nm++;
+        auto blog = [&](double v, double lo, double hi) __attribute__((always_inline)) {
+            if (gb(lo)) { if (v - lo <= 0) bad = 1; else bar -= log(v - lo); }
+            if (gb(hi)) { if (hi - v <= 0) bad = 1; else bar -= log(hi - v); }
+            if (gb(lo) && !gb(hi)) lin += v - lo;
+            if (gb(hi) && !gb(lo)) lin += hi - v;
+        };
+        for (int e = lane + NX; e < (N + 1) * NX; e += 64) blog(x[e], P.x_lo[e % NX], P.x_hi[e % NX]);
+        for (int e = lane; e < N * NU; e += 64)
+            if (!ufix(e)) blog(u[e], ulo[e], uhi[e]);
+        for (int e = lane; e < N * NI; e += 64) blog(s[(e / NI) * NIA + e % NI], clo[e], chi[e]);
+        fs = wave_sum(fs); t = wave_sum(t); bar = wave_sum(bar); lin = wave_sum(lin); bad = wave_sum_i(bad);
+        phi = fs + mu_o * bar + KAPPA_D * mu_o * lin;
+        th = t;
+        okp = bad == 0;
+    };
+
+    if constexpr (PH == 0) {
+    if (flt && st.pend == GP_RESTO) {
+        // ---------------- MinC_1NrmRestorationPhase / RestoIterateInitializer at the current point
+        double cm = 0.0;
+        for (int e = lane; e < N * NX; e += 64) cm = fmax(cm, fabs(R(e / NX)[D::O_F + e % NX] - x[(e / NX + 1) * NX + e % NX]));
+        for (int r = lane; r < NRI; r += 64) {
+            if (!el_on(r)) continue;
+            double c;
+            if ((size_t)r < NRo) c = R(r / NIA)[D::O_CI + r % NIA] - s[r];
+            else {
+                const int e = r - (int)NRo, k = e / NET, ee = e % NET;
+                c = ee < NEA ? R(k)[D::O_CE + ee] : R(k)[D::O_CM + ee - NEA];
+            }
+            cm = fmax(cm, fabs(c));
         }
-    if (NM > 0)
-        for (int e = lane; e < N * NM; e += 64) {
-            const int k = e / NM, m = e % NM;
-            pinf = fmax(pinf, fabs(R(k)[D::O_CM + m]));
-            sm += fabs(ye[k * NET + NEA + m]);
-            nm++;
+        cm = wave_max(cm);
+        const double mu_r = fmax(mu, cm);
+        for (int r = lane; r < NRI; r += 64) {
+            if (!el_on(r)) { prr[r] = nrr[r] = 1.0; zpr[r] = znr[r] = 0.0; continue; }
+            double c;
+            if ((size_t)r < NRo) c = R(r / NIA)[D::O_CI + r % NIA] - s[r];
+            else {
+                const int e = r - (int)NRo, k = e / NET, ee = e % NET;
+                c = ee < NEA ? R(k)[D::O_CE + ee] : R(k)[D::O_CM + ee - NEA];
+            }
+            const double a = (mu_r - RHO_R * c) / (2.0 * RHO_R);
+            nrr[r] = a + sqrt(a * a + mu_r * c / (2.0 * RHO_R));
+            prr[r] = c + nrr[r];
+            zpr[r] = mu_r / prr[r];
+            znr[r] = mu_r / nrr[r];
         }
-    dinf = wave_max(dinf); pinf = wave_max(pinf); cinf0 = wave_max(cinf0); cinfm = wave_max(cinfm);
-    sm = wave_sum(sm); sbm = wave_sum(sbm); nm = wave_sum_i(nm); nbm = wave_sum_i(nbm);
-    const double sd = fmax(s_max, (sm + sbm) / fmax(1.0, (double)(nm + nbm))) / s_max;
-    const double sc = fmax(s_max, sbm / fmax(1.0, (double)nbm)) / s_max;
-    const double E0 = fmax(fmax(dinf / sd, pinf), cinf0 / sc);
+        for (int e = lane; e < (int)Z.x(); e += 64) { wR[e] = x[e]; dR[e] = 1.0 / fmax(1.0, x[e] * x[e]); }
+        for (int e = lane; e < N * NU; e += 64) { wR[Z.x() + e] = u[e]; dR[Z.x() + e] = 1.0 / fmax(1.0, u[e] * u[e]); }
+        for (int e = lane; e < (int)Z.x(); e += 64) { zxL[e] = fmin(zxL[e], RHO_R); zxU[e] = fmin(zxU[e], RHO_R); }
+        for (int e = lane; e < N * NU; e += 64) { zuL[e] = fmin(zuL[e], RHO_R); zuU[e] = fmin(zuU[e], RHO_R); }
+        for (int e = lane; e < N * NIA; e += 64) { vL[e] = fmin(vL[e], RHO_R); vU[e] = fmin(vU[e], RHO_R); }
+        // least-square multipliers (DefaultIterateInitializer::least_square_mults): the system [[I, J^T], [J, 0]]
+        // through the stage factorisation -- Sigma = 0 (x_N: I), slacks and elastic variables with unit
+        // Hessian, gradients grad f_R - z (grad f_R = 0 at w_R), zero constraint residuals and multipliers
+        for (int e = lane; e < (N + 1) * NX; e += 64) {
+            const int k = e / NX;
+            Sx[e] = (k == N) ? 1.0 : 0.0;
+            gx[e] = k > 0 ? -zxL[e] + zxU[e] : 0.0;
+        }
+        for (int e = lane; e < N * NU; e += 64) { Su[e] = 0.0; gu[e] = ufix(e) ? 0.0 : -zuL[e] + zuU[e]; }
+        for (int e = lane; e < N * NIA; e += 64) { Ss[e] = 1.0; gs[e] = -vL[e] + vU[e]; }
+        for (int r = lane; r < NRI; r += 64) {
+            const bool on = el_on(r);
+            Spr[r] = Snr[r] = on ? 1.0 : INFINITY;
+            gpr[r] = -zpr[r];
+            gnr[r] = -znr[r];
+            rowr[r] = on ? znr[r] - zpr[r] : 0.0;
+        }
+        for (int e = lane; e < N * NX; e += 64) { lam[e] = 0.0; rdyn[e] = 0.0; }
+        for (int e = lane; e < N * NIA; e += 64) { yi[e] = 0.0; rin[e] = 0.0; }
+        for (int e = lane; e < N * NET; e += 64) { ye[e] = 0.0; req[e] = 0.0; }
+        gsync();
+        if (lane == 0) {
+            st.mu_orig = mu;
+            st.mu = mu_r;
+            st.zeta = sqrt(mu_r);
+            st.mode = 1;
+            st.ic_last_main = st.ic_last;
+            st.ic_last = 0.0;
+            st.nf[1] = 0;
+            st.thm[1][0] = st.thm[1][1] = -1.0;
+            st.in_wd = 0; st.wd_short = 0; st.in_soft = 0; st.soft_cnt = 0;
+            st.n_resto++;
+            st.pend = GP_LSM;
+            A.st[b] = st;
+        }
+        return;
+    }
+    // ---------------- optimality error (IPOPT E_0, s_max scaling)
+    const GErr Eq = opt_err(mu);
+    const double dinf = Eq.dinf, pinf = Eq.pinf, sd = Eq.sd, sc = Eq.sc;
+    double cinfm = Eq.cinfm;
+    const double E0 = fmax(fmax(dinf / sd, pinf), Eq.cinf0 / sc);
     double Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
+    if (flt && st.pend == GP_SOFT) {  // TrySoftRestoStep, second half: the pending step's primal-dual error
+        if (Eq.s1 / Eq.n1 <= 0.9999 * st.pd_cur) {
+            st.pend = GP_NONE;
+            st.n_soft++;
+        } else {  // undo the step; the restoration phase starts from the point it was taken at
+            const GSz<D> &Zc = Z;
+            double *arr[16] = {x, u, s, lam, ye, yi, zxL, zxU, zuL, zuU, vL, vU, prr, nrr, zpr, znr};
+            const size_t len[16] = {Zc.x(), Zc.u(), Zc.i(), Zc.l(), Zc.e(), Zc.i(), Zc.x(), Zc.x(), Zc.u(), Zc.u(),
+                                    Zc.i(), Zc.i(), Zc.nr(), Zc.nr(), Zc.nr(), Zc.nr()};
+            const double *src = A.wdit + b * Z.bk();
+            size_t off = 0;
+            for (int a = 0; a < 12; a++) {
+                for (size_t e = lane; e < len[a]; e += 64) arr[a][e] = src[off + e];
+                off += len[a];
+            }
+            gsync();
+            if (lane == 0) {
+                st.in_soft = 0;
+                st.soft_cnt = 0;
+                st.pend = GP_IDLE_RESTO;
+                A.st[b] = st;
+            }
+            return;
+        }
+    }
     st.E0 = E0;
     st.cviol = pinf;
-    if (E0 <= P.tol && pinf <= P.constr_viol_tol) { finish(GS_CONVERGED); return; }
+    if (!rsm) {
+        if (E0 <= P.tol && pinf <= P.constr_viol_tol) { finish(GS_CONVERGED); return; }
+    } else {
+        // RestoFilterConvergenceCheck: the main problem's filter and its reference point accept the iterate and
+        // theta fell to kappa_resto = 0.9 of its value where the restoration started
+        double pho, tho;
+        bool oko;
+        orig_merit_cur(st.mu_orig, pho, tho, oko);
+        const bool cur_ok = (tho - (1.0 - 1e-5) * st.rs_th <= 10.0 * 2.220446049250313e-16 * fabs(st.rs_th)) ||
+                            ((pho - st.rs_ph) - (-1e-8 * st.rs_th) <= 10.0 * 2.220446049250313e-16 * fabs(st.rs_ph));
+        if (oko && isfinite(pho) && tho <= 0.9 * st.rs_th && cur_ok && fil_ok(0, pho, tho)) {
+            // back to the main problem: y = 0 (constr_mult_reset_threshold = 0), bound multipliers reset to 1
+            // when any exceeds bound_mult_reset_threshold = 1000
+            double zm = 0.0;
+            for (int e = lane; e < (int)Z.x(); e += 64) zm = fmax(zm, fmax(zxL[e], zxU[e]));
+            for (int e = lane; e < N * NU; e += 64) zm = fmax(zm, fmax(zuL[e], zuU[e]));
+            for (int e = lane; e < N * NIA; e += 64) zm = fmax(zm, fmax(vL[e], vU[e]));
+            zm = wave_max(zm);
+            if (zm > 1e3) {
+                for (int e = lane; e < (int)Z.x(); e += 64) { if (zxL[e] > 0.0) zxL[e] = 1.0; if (zxU[e] > 0.0) zxU[e] = 1.0; }
+                for (int e = lane; e < N * NU; e += 64) { if (zuL[e] > 0.0) zuL[e] = 1.0; if (zuU[e] > 0.0) zuU[e] = 1.0; }
+                for (int e = lane; e < N * NIA; e += 64) { if (vL[e] > 0.0) vL[e] = 1.0; if (vU[e] > 0.0) vU[e] = 1.0; }
+            }
+            for (int e = lane; e < N * NX; e += 64) lam[e] = 0.0;
+            for (int e = lane; e < N * NIA; e += 64) yi[e] = 0.0;
+            for (int e = lane; e < N * NET; e += 64) ye[e] = 0.0;
+            gsync();
+            if (lane == 0) {
+                st.mode = 0;
+                st.mu = st.mu_orig;
+                st.ic_last = st.ic_last_main;
+                st.in_wd = 0; st.wd_short = 0; st.in_soft = 0; st.soft_cnt = 0;
+                st.pend = GP_IDLE;
+                A.st[b] = st;
+            }
+            return;
+        }
+        if (E0 <= P.tol) { finish(GS_LOCINF); return; }
+    }
     if (st.iter >= P.max_iter) { finish(GS_MAXITER); return; }
-    while (Emu <= kappa_eps * mu && mu > P.tol / 10.0) {
-        const double mnew = fmax(P.tol / 10.0, fmin(kappa_mu * mu, pow(mu, theta_mu)));
+    const double mu_min = flt ? P.tol / (kappa_eps + 1.0) : P.tol / 10.0;
+    while (Emu <= kappa_eps * mu && mu > mu_min) {
+        const double mnew = fmax(mu_min, fmin(kappa_mu * mu, pow(mu, theta_mu)));
         if (mnew >= mu) break;
         mu = mnew;
-        double cm = 0.0;
+        if (flt) {  // MonotoneMuUpdate resets the line search's filter; the proximity weight follows mu
+            st.nf[st.mode] = 0;
+            if (rsm) st.zeta = sqrt(mu);
+        }
+        double cmx = 0.0;
         for (int e = lane; e < N * NX; e += 64) {
             const int i = e + NX, j = e % NX;
-            if (gb(P.x_lo[j])) cm = fmax(cm, fabs(zxL[i] * (x[i] - P.x_lo[j]) - mu));
-            if (gb(P.x_hi[j])) cm = fmax(cm, fabs(zxU[i] * (P.x_hi[j] - x[i]) - mu));
+            if (gb(P.x_lo[j])) cmx = fmax(cmx, fabs(zxL[i] * (x[i] - P.x_lo[j]) - mu));
+            if (gb(P.x_hi[j])) cmx = fmax(cmx, fabs(zxU[i] * (P.x_hi[j] - x[i]) - mu));
         }
         for (int e = lane; e < N * NU; e += 64) {
             if (ufix(e)) continue;
-            if (gb(ulo[e])) cm = fmax(cm, fabs(zuL[e] * (u[e] - ulo[e]) - mu));
-            if (gb(uhi[e])) cm = fmax(cm, fabs(zuU[e] * (uhi[e] - u[e]) - mu));
+            if (gb(ulo[e])) cmx = fmax(cmx, fabs(zuL[e] * (u[e] - ulo[e]) - mu));
+            if (gb(uhi[e])) cmx = fmax(cmx, fabs(zuU[e] * (uhi[e] - u[e]) - mu));
         }
         for (int e = lane; e < N * NI; e += 64) {
             const int i = (e / NI) * NIA + e % NI;
-            if (gb(clo[e])) cm = fmax(cm, fabs(vL[i] * (s[i] - clo[e]) - mu));
-            if (gb(chi[e])) cm = fmax(cm, fabs(vU[i] * (chi[e] - s[i]) - mu));
+            if (gb(clo[e])) cmx = fmax(cmx, fabs(vL[i] * (s[i] - clo[e]) - mu));
+            if (gb(chi[e])) cmx = fmax(cmx, fabs(vU[i] * (chi[e] - s[i]) - mu));
         }
-        cinfm = wave_max(cm);
+        if (rsm)
+            for (int r = lane; r < NRI; r += 64)
+                if (el_on(r)) cmx = fmax(cmx, fmax(fabs(zpr[r] * prr[r] - mu), fabs(znr[r] * nrr[r] - mu)));
+        cinfm = wave_max(cmx);
         Emu = fmax(fmax(dinf / sd, pinf), cinfm / sc);
     }
     GSTAMP(0);
 
     // ---------------- barrier Sigma / gradients, residuals of the current point
+    const double kd = flt ? KAPPA_D * mu : 0.0;  // IPOPT kappa_d: linear damping of single-bounded variables
     for (int e = lane; e < (N + 1) * NX; e += 64) {
         const int k = e / NX, j = e % NX;
         double sg = 0, g = 0;
         if (k > 0) {
             if (gb(P.x_lo[j])) { sg += zxL[e] / (x[e] - P.x_lo[j]); g -= mu / (x[e] - P.x_lo[j]); }
             if (gb(P.x_hi[j])) { sg += zxU[e] / (P.x_hi[j] - x[e]); g += mu / (P.x_hi[j] - x[e]); }
+            if (flt && gb(P.x_lo[j]) && !gb(P.x_hi[j])) g += kd;
+            if (flt && gb(P.x_hi[j]) && !gb(P.x_lo[j])) g -= kd;
+            if (rsm) { sg += st.zeta * dR[e]; g += st.zeta * dR[e] * (x[e] - wR[e]); }
         }
         Sx[e] = sg;
         gx[e] = g;
@@ -582,6 +899,9 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         if (!ufix(e)) {
             if (gb(ulo[e])) { sg += zuL[e] / (u[e] - ulo[e]); g -= mu / (u[e] - ulo[e]); }
             if (gb(uhi[e])) { sg += zuU[e] / (uhi[e] - u[e]); g += mu / (uhi[e] - u[e]); }
+            if (flt && gb(ulo[e]) && !gb(uhi[e])) g += kd;
+            if (flt && gb(uhi[e]) && !gb(ulo[e])) g -= kd;
+            if (rsm) { sg += st.zeta * dR[Z.x() + e]; g += st.zeta * dR[Z.x() + e] * (u[e] - wR[Z.x() + e]); }
         }
         Su[e] = sg;
         gu[e] = g;
@@ -591,15 +911,29 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         double sg = 0, g = 0;
         if (gb(clo[e])) { sg += vL[i] / (s[i] - clo[e]); g -= mu / (s[i] - clo[e]); }
         if (gb(chi[e])) { sg += vU[i] / (chi[e] - s[i]); g += mu / (chi[e] - s[i]); }
+        if (flt && gb(clo[e]) && !gb(chi[e])) g += kd;
+        if (flt && gb(chi[e]) && !gb(clo[e])) g -= kd;
         Ss[i] = sg;
         gs[i] = g;
-        rin[i] = cact(k, q) ? R(k)[D::O_CI + q] - s[i] : 0.0;
+        rin[i] = cact(k, q) ? R(k)[D::O_CI + q] - s[i] + (rsm ? nrr[i] - prr[i] : 0.0) : 0.0;
     }
     for (int e = lane; e < N * NX; e += 64) rdyn[e] = R(e / NX)[D::O_F + e % NX] - x[(e / NX + 1) * NX + e % NX];
     for (int e = lane; e < N * NET; e += 64) {
         const int k = e / NET, ee = e % NET;
-        req[e] = ee < NEA ? ((ee < NE && eqon(k)) ? R(k)[D::O_CE + ee] : 0.0) : R(k)[D::O_CM + ee - NEA];
+        double v = ee < NEA ? ((ee < NE && eqon(k)) ? R(k)[D::O_CE + ee] : 0.0) : R(k)[D::O_CM + ee - NEA];
+        if (rsm && el_on((int)NRo + e)) v += nrr[NRo + e] - prr[NRo + e];
+        req[e] = v;
     }
+    if (rsm)  // the elastic variables condensed: Sp dp = dy - r_p, Sn dn = -dy - r_n (oracle barrier_f)
+        for (int r = lane; r < NRI; r += 64) {
+            if (!el_on(r)) { Spr[r] = Snr[r] = INFINITY; gpr[r] = gnr[r] = rowr[r] = 0.0; continue; }
+            const double y = el_y(r);
+            Spr[r] = zpr[r] / prr[r];
+            Snr[r] = znr[r] / nrr[r];
+            gpr[r] = -mu / prr[r] + kd;
+            gnr[r] = -mu / nrr[r] + kd;
+            rowr[r] = (RHO_R + gpr[r] - y) / Spr[r] - (RHO_R + gnr[r] + y) / Snr[r];
+        }
     gsync();
     GSTAMP(1);
     GSTAMP_FLUSH;
@@ -613,8 +947,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
 
     // ---------------- Riccati factorisation with inertia test (stage blocks [[Quu, Du^T], [Du, -dc]])
     double dw_c = 0.0, dc_c = 0.0;
+    // the least-square multiplier pass of a restoration start: the stage Hessians are identities and the
+    // objective gradient is left out
+    const bool lsm = flt && st.pend == GP_LSM;
+    auto rdiag = [&](size_t r) __attribute__((always_inline)) -> double { return rsm ? 1.0 / Spr[r] + 1.0 / Snr[r] : 0.0; };
     // stage k's A, B, J_I, J_M (and W into Hs), J_E of node k+1, the fixed-control and active-row flags
-    auto stage_in = [&](int k, bool withW) {
+    auto stage_in = [&](int k, bool withW) __attribute__((always_inline)) {
         const double *rk = R(k);
         const bool en = eqon(k + 1);
         glds_copy(Ab, rk + D::O_A, NX * NX);
@@ -628,7 +966,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
         for (int q = lane; q < NI; q += 64) acts[q] = cact(k, q) ? 1 : 0;
     };
-    auto factor = [&](double dw, double dc, double d1) -> int {
+    auto factor = [&](double dw, double dc, double d1) __attribute__((always_inline)) -> int {
         for (int e = lane; e < NX * NX; e += 64) Ps[e] = (e / NX == e % NX) ? Sx[N * NX + e / NX] + dw : 0.0;
         __syncthreads();
         for (int k = N - 1; k >= 0; k--) {
@@ -642,8 +980,10 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             gsync();
             for (int q = lane; q < NI; q += 64) {
                 const double sg = Vs[V_SS + q] + dw;
-                Dds[q] = acts[q] ? sg / (1.0 + dc * sg) : 0.0;
+                Dds[q] = acts[q] ? sg / (1.0 + (dc + rdiag((size_t)k * NIA + q)) * sg) : 0.0;
             }
+            if (lsm)
+                for (int e = lane; e < NV * NV; e += 64) Hs[e] = (e / NV == e % NV) ? 1.0 : 0.0;
             gsync();
             GSTAMP(8);
             // H = W + J_I^T D J_I (+ diagonal terms), in place over W (each lane its own tile)
@@ -685,7 +1025,9 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (a < NU && c < NU) {
                     continue;  // the control block: tile_gemm above
                 } else if (a >= NU && c >= NU) {
-                    v = (a == c) ? ((a - NU >= NEA || (en && a - NU < NE)) ? -dc : -1.0) : 0.0;
+                    const int ee = a - NU;
+                    const size_t rr = NRo + (size_t)(ee >= NEA ? k : k + 1) * NET + ee;
+                    v = (a == c) ? ((ee >= NEA || (en && ee < NE)) ? -dc - rdiag(rr) : -1.0) : 0.0;
                 } else {
                     const int ee = (a >= NU ? a : c) - NU, uu = a >= NU ? c : a;
                     if (fixs[uu]) v = 0.0;
@@ -772,7 +1114,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     };
 
     // ---------------- direction for constraint residuals (rd, ri, re) with the stored factorisation
-    auto direction = [&](const double *rd, const double *ri, const double *re) {
+    auto direction = [&](const double *rd, const double *ri, const double *re) __attribute__((always_inline)) {
         const double dw = dw_c, dc = dc_c;
         for (int j = lane; j < NX; j += 64) pvs[j] = gx[N * NX + j] - lam[(N - 1) * NX + j];
         gsync();
@@ -815,8 +1157,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 const int i = k * NIA + q;
                 double w = yi[i];
                 if (cact(k, q)) {
-                    const double sg = Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
-                    w += Dd * (ri[i] + (gs[i] - yi[i]) / sg);
+                    const double sg = Ss[i] + dw, Dd = sg / (1.0 + (dc + rdiag(i)) * sg);
+                    w += Dd * (ri[i] + (rsm ? rowr[i] : 0.0) + (gs[i] - yi[i]) / sg);
                 }
                 Vs[V_W + q] = w;
             }
@@ -826,7 +1168,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 const bool fa = a < NX ? (k == 0) : fixs[a - NX];
                 double g = 0.0;
                 if (!fa) {
-                    g = Vs[V_GL + a];
+                    g = lsm ? 0.0 : Vs[V_GL + a];
                     for (int q = 0; q < NI; q++) g += JIs[q * NV + a] * Vs[V_W + q];
                     if (a < NX) {
                         g += Vs[V_GX + a] - Vs[V_LP + a];
@@ -857,9 +1199,11 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                     }
                 } else if (a - NU >= NEA) {
                     z = Vs[V_RE + a - NU];  // mixed row of stage k
+                    if (rsm) z += rowr[NRo + (size_t)k * NET + a - NU];
                 } else if (en && a - NU < NE) {
                     const int ee = a - NU;
                     z = Vs[V_RN + ee];
+                    if (rsm) z += rowr[NRo + (size_t)(k + 1) * NET + ee];
                     for (int l = 0; l < NX; l++) z += Jn[ee * NX + l] * Vs[V_RD + l];
                 }
                 zv[a] = z;
@@ -941,8 +1285,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 double jd = 0.0;
                 for (int a = 0; a < NX; a++) jd += rk[D::O_JI + q * NV + a] * dx[k * NX + a];
                 for (int a = 0; a < NU; a++) jd += rk[D::O_JI + q * NV + NX + a] * du[k * NU + a];
-                const double sg = Ss[i] + dw, Dd = sg / (1.0 + dc * sg), rs = gs[i] - yi[i];
-                dyv = Dd * (jd + ri[i] + rs / sg);
+                const double sg = Ss[i] + dw, Dd = sg / (1.0 + (dc + rdiag(i)) * sg), rs = gs[i] - yi[i];
+                dyv = Dd * (jd + ri[i] + (rsm ? rowr[i] : 0.0) + rs / sg);
                 dsv = (dyv - rs) / sg;
             }
             dyi[i] = dyv;
@@ -976,13 +1320,23 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             dvL[i] = a;
             dvU[i] = c;
         }
+        if (rsm)  // elastic variables: Sp dp = dy - r_p, Sn dn = -dy - r_n, and their bound multipliers
+            for (int r = lane; r < NRI; r += 64) {
+                if (!el_on(r)) { dpr[r] = dnr[r] = dzp[r] = dzn[r] = 0.0; continue; }
+                const double dy = (size_t)r < NRo ? dyi[r] : dye[r - NRo], y = el_y(r);
+                const double rp = RHO_R + gpr[r] - y, rn = RHO_R + gnr[r] + y;
+                dpr[r] = (dy - rp) / Spr[r];
+                dnr[r] = (-dy - rn) / Snr[r];
+                dzp[r] = mu / prr[r] - zpr[r] - zpr[r] / prr[r] * dpr[r];
+                dzn[r] = mu / nrr[r] - znr[r] - znr[r] / nrr[r] * dnr[r];
+            }
         gsync();
         GSTAMP(18);
     };
 
-    auto ftb = [&](double &ap_o, double &az_o) {
+    auto ftb = [&](double &ap_o, double &az_o) __attribute__((always_inline)) {
         double ap = 1.0, az = 1.0;
-        auto one = [&](double v, double dv, double lo, double hi, double zl, double dzl, double zu, double dzu) {
+        auto one = [&](double v, double dv, double lo, double hi, double zl, double dzl, double zu, double dzu) __attribute__((always_inline)) {
             if (gb(lo)) {
                 if (dv < 0) ap = fmin(ap, -tau_fb * (v - lo) / dv);
                 if (dzl < 0) az = fmin(az, -tau_fb * zl / dzl);
@@ -1002,15 +1356,22 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             const int i = (e / NI) * NIA + e % NI;
             one(s[i], ds[i], clo[e], chi[e], vL[i], dvL[i], vU[i], dvU[i]);
         }
+        if (rsm)
+            for (int r = lane; r < NRI; r += 64)
+                if (el_on(r)) {
+                    one(prr[r], dpr[r], 0.0, INFINITY, zpr[r], dzp[r], 0.0, 0.0);
+                    one(nrr[r], dnr[r], 0.0, INFINITY, znr[r], dzn[r], 0.0, 0.0);
+                }
         ap_o = wave_min(ap);
         az_o = wave_min(az);
     };
 
     // barrier objective + l1 violation at (xx, uu, ss): cur = the current point (values in the records)
     auto merit = [&](const double *xx, const double *uu, const double *ss, bool cur, double *trd, double *tri,
-                     double *tre, double &phi, double &th, bool &okp) {
-        double fs = 0.0, t = 0.0, bar = 0.0;
+                     double *tre, double &phi, double &th, bool &okp) __attribute__((always_inline)) {
+        double fs = 0.0, t = 0.0, bar = 0.0, lin = 0.0;
         int bad = 0;
+        const double *pe = cur ? prr : tpr, *ne_ = cur ? nrr : tnr;  // elastic variables of the point (rsm)
         for (int k = lane; k < N; k += 64) {
             double l, ci[NIA], ce[NET], f[NX];
             if (cur) {
@@ -1023,61 +1384,102 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             } else {
                 FAM::values(M, F, P, xx + (size_t)k * NX, uu + (size_t)k * NU, lref, l, ci, ce, f);
             }
-            fs += l;
+            if (!rsm) fs += l;
             for (int j = 0; j < NX; j++) {
                 const double r = f[j] - xx[(k + 1) * NX + j];
                 t += fabs(r);
                 if (trd) trd[k * NX + j] = r;
             }
             for (int q = 0; q < NI; q++) {
-                const double r = cact(k, q) ? ci[q] - ss[k * NIA + q] : 0.0;
+                const int i = k * NIA + q;
+                const double r = cact(k, q) ? ci[q] - ss[i] + (rsm ? ne_[i] - pe[i] : 0.0) : 0.0;
                 t += fabs(r);
-                if (tri) tri[k * NIA + q] = r;
+                if (tri) tri[i] = r;
             }
             const bool eo = eqon(k);
             for (int ee = 0; ee < NEA; ee++) {
-                const double r = (eo && ee < NE) ? ce[ee] : 0.0;
+                const size_t rr = NRo + (size_t)k * NET + ee;
+                const double r = (eo && ee < NE) ? ce[ee] + (rsm ? ne_[rr] - pe[rr] : 0.0) : 0.0;
                 t += fabs(r);
                 if (tre) tre[k * NET + ee] = r;
             }
             for (int m = 0; m < NM; m++) {  // families write the mixed rows after their NE state rows
-                const double r = ce[NE + m];
+                const size_t rr = NRo + (size_t)k * NET + NEA + m;
+                const double r = ce[NE + m] + (rsm ? ne_[rr] - pe[rr] : 0.0);
                 t += fabs(r);
                 if (tre) tre[k * NET + NEA + m] = r;
             }
         }
-        auto blog = [&](double v, double lo, double hi) {
+        auto blog = [&](double v, double lo, double hi) __attribute__((always_inline)) {
             if (gb(lo)) { if (v - lo <= 0) bad = 1; else bar -= log(v - lo); }
             if (gb(hi)) { if (hi - v <= 0) bad = 1; else bar -= log(hi - v); }
+            if (flt && gb(lo) && !gb(hi)) lin += v - lo;
+            if (flt && gb(hi) && !gb(lo)) lin += hi - v;
         };
         for (int e = lane + NX; e < (N + 1) * NX; e += 64) blog(xx[e], P.x_lo[e % NX], P.x_hi[e % NX]);
         for (int e = lane; e < N * NU; e += 64)
             if (!ufix(e)) blog(uu[e], ulo[e], uhi[e]);
         for (int e = lane; e < N * NI; e += 64) blog(ss[(e / NI) * NIA + e % NI], clo[e], chi[e]);
+        if (rsm) {  // restoration objective: rho sum(p + n) + zeta/2 |D_R (w - w_R)|^2, barrier and damping on p, n
+            double pn = 0.0, prox = 0.0;
+            for (int r = lane; r < NRI; r += 64)
+                if (el_on(r)) {
+                    pn += pe[r] + ne_[r];
+                    if (pe[r] <= 0 || ne_[r] <= 0) bad = 1;
+                    else bar -= log(pe[r]) + log(ne_[r]);
+                }
+            for (int e = lane + NX; e < (N + 1) * NX; e += 64) prox += dR[e] * (xx[e] - wR[e]) * (xx[e] - wR[e]);
+            for (int e = lane; e < N * NU; e += 64)
+                if (!ufix(e)) prox += dR[Z.x() + e] * (uu[e] - wR[Z.x() + e]) * (uu[e] - wR[Z.x() + e]);
+            fs += RHO_R * pn + 0.5 * st.zeta * prox;
+            lin += pn;
+        }
         fs = wave_sum(fs);
         t = wave_sum(t);
         bar = wave_sum(bar);
         bad = wave_sum_i(bad);
         phi = fs + mu * bar;
+        if (flt) phi += KAPPA_D * mu * wave_sum(lin);
         th = t;
         okp = bad == 0;
         gsync();
     };
-    auto trial = [&](double al) {
+    auto trial = [&](double al) __attribute__((always_inline)) {
         for (int e = lane; e < (N + 1) * NX; e += 64) tx[e] = x[e] + al * dx[e];
         for (int e = lane; e < N * NU; e += 64) tu[e] = u[e] + al * du[e];
         for (int e = lane; e < N * NIA; e += 64) ts[e] = s[e] + al * ds[e];
+        if (rsm)
+            for (int r = lane; r < NRI; r += 64) { tpr[r] = prr[r] + al * dpr[r]; tnr[r] = nrr[r] + al * dnr[r]; }
         gsync();
     };
     // direction arrays (save / restore around second-order corrections)
-    auto dir_copy = [&](bool save) {
-        double *arr[12] = {dx, du, ds, dlam, dye, dyi, dzxL, dzxU, dzuL, dzuU, dvL, dvU};
-        const size_t len[12] = {Z.x(), Z.u(), Z.i(), Z.l(), Z.e(), Z.i(), Z.x(), Z.x(), Z.u(), Z.u(), Z.i(), Z.i()};
+    // the direction's / the iterate's arrays (with the elastic variables in the restoration phase) to / from buf
+    auto dir_copy_to = [&](double *buf, bool save) __attribute__((always_inline)) {
+        double *arr[16] = {dx, du, ds, dlam, dye, dyi, dzxL, dzxU, dzuL, dzuU, dvL, dvU, dpr, dnr, dzp, dzn};
+        const size_t len[16] = {Z.x(), Z.u(), Z.i(), Z.l(), Z.e(), Z.i(), Z.x(), Z.x(), Z.u(), Z.u(), Z.i(), Z.i(),
+                                Z.nr(), Z.nr(), Z.nr(), Z.nr()};
         size_t off = 0;
-        for (int a = 0; a < 12; a++) {
+        const int na = rsm ? 16 : 12;
+        for (int a = 0; a < na; a++) {
             for (size_t e = lane; e < len[a]; e += 64) {
-                if (save) bkp[off + e] = arr[a][e];
-                else arr[a][e] = bkp[off + e];
+                if (save) buf[off + e] = arr[a][e];
+                else arr[a][e] = buf[off + e];
+            }
+            off += len[a];
+        }
+        gsync();
+    };
+    auto dir_copy = [&](bool save) __attribute__((always_inline)) { dir_copy_to(bkp, save); };
+    auto iter_copy_to = [&](double *buf, bool save) __attribute__((always_inline)) {
+        double *arr[16] = {x, u, s, lam, ye, yi, zxL, zxU, zuL, zuU, vL, vU, prr, nrr, zpr, znr};
+        const size_t len[16] = {Z.x(), Z.u(), Z.i(), Z.l(), Z.e(), Z.i(), Z.x(), Z.x(), Z.u(), Z.u(), Z.i(), Z.i(),
+                                Z.nr(), Z.nr(), Z.nr(), Z.nr()};
+        size_t off = 0;
+        const int na = rsm ? 16 : 12;
+        for (int a = 0; a < na; a++) {
+            for (size_t e = lane; e < len[a]; e += 64) {
+                if (save) buf[off + e] = arr[a][e];
+                else arr[a][e] = buf[off + e];
             }
             off += len[a];
         }
@@ -1085,20 +1487,34 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     };
 
     if constexpr (PH == 1) {
-    // ---------------- inertia correction
-    double dw = 0.0, dc = P.dc_always ? 1e-8 * pow(mu, 0.25) : 0.0, d1 = 0.0;
+    if (flt && (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO)) return;
+    // ---------------- inertia correction.  Merit mode: DESIGN.md section 4 (tiers).  IPOPT mode
+    // (IpPDPerturbationHandler.cpp, oracle/mf_ocp.c factor_f): delta_w = 0 first; on wrong inertia 1e-4 if no
+    // earlier perturbation, else max(1e-20, last / 3); then x100 (no earlier one, or last far below) or x8 up to
+    // 1e40.  A singular matrix first gets delta_c = 1e-8 mu^(1/4).  The least-square multiplier pass of a
+    // restoration start factors once, unperturbed.  (One factor / direction call site: the kernel's registers.)
+    double dw = 0.0, dc = (P.dc_always && !lsm) ? 1e-8 * pow(mu, 0.25) : 0.0, d1 = 0.0;
     int tier = st.reg_tier, step_no = 0;
     double reg = (st.reg_tier == 0) ? 0.0 : st.reg_last / 3.0;
     if (st.reg_tier != 0 && reg < 1e-8) { tier = 0; reg = 0.0; }
     if (tier == 1) d1 = reg; else if (tier == 2) dw = reg;
+    if (flt) { dw = 0.0; d1 = 0.0; }
     const bool has_t1 = P.tier1_to > P.tier1_from;
     bool factor_ok = false;
-    for (int tries = 0; tries < 60; tries++) {
+    const int max_tries = flt ? 200 : 60;
+    for (int tries = 0; tries < max_tries; tries++) {
         GSTAMP_COUNT(20, 1);
         const int fr = factor(dw, dc, d1);
         if (fr == 0) { factor_ok = true; break; }
+        if (lsm) break;
         if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
         st.n_ic++;
+        if (flt) {
+            if (dw == 0.0) dw = (st.ic_last == 0.0) ? 1e-4 : fmax(1e-20, st.ic_last / 3.0);
+            else dw *= (st.ic_last == 0.0 || 1e5 * st.ic_last < dw) ? 100.0 : 8.0;
+            if (dw > 1e40) break;
+            continue;
+        }
         step_no++;
         if (tier == 0) {
             tier = has_t1 ? 1 : 2;
@@ -1113,13 +1529,22 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         d1 = (tier == 1) ? reg : 0.0;
         dw = (tier == 2) ? reg : 0.0;
     }
-    if (!factor_ok) { finish(GS_INERTIA); return; }
-    st.reg_tier = tier;
-    st.reg_last = reg;
-    dw_c = dw;
-    dc_c = dc;
+    if (!factor_ok && !lsm) { finish(GS_INERTIA); return; }
+    if (lsm) {
+        dw_c = 0.0;
+        dc_c = factor_ok ? 0.0 : -1.0;  // -1: singular system, the multipliers stay 0 (k_gls)
+    } else {
+        if (flt) {
+            if (dw > 0.0) st.ic_last = dw;
+        } else {
+            st.reg_tier = tier;
+            st.reg_last = reg;
+        }
+        dw_c = dw;
+        dc_c = dc;
+    }
     GSTAMP(2);
-    direction(rdyn, rin, req);
+    if (factor_ok) direction(rdyn, rin, req);
     GSTAMP(3);
     GSTAMP_FLUSH;
     if (lane == 0) {
@@ -1133,6 +1558,280 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     // ---------------- step, line search with second-order corrections, update
     dw_c = st.dw_c;
     dc_c = st.dc_c;
+    if (flt) {
+    // ================= IPOPT's FindAcceptableTrialPoint (oracle/mf_ocp.c ipm_filter / filter_backtrack)
+    if (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO) {
+        if (lane == 0) {
+            st.pend = st.pend == GP_IDLE_RESTO ? GP_RESTO : GP_NONE;
+            st.iter++;
+            A.st[b] = st;
+        }
+        return;
+    }
+    if (lsm) {  // least-square multipliers of the restoration start: 0 if singular or max |y| > 1000
+        double ym = 0.0;
+        for (int e = lane; e < N * NX; e += 64) ym = fmax(ym, fabs(dlam[e]));
+        for (int e = lane; e < N * NIA; e += 64) ym = fmax(ym, fabs(dyi[e]));
+        for (int e = lane; e < N * NET; e += 64) ym = fmax(ym, fabs(dye[e]));
+        ym = wave_max(ym);
+        if (dc_c == 0.0 && ym <= 1e3) {
+            for (int e = lane; e < N * NX; e += 64) lam[e] = dlam[e];
+            for (int e = lane; e < N * NIA; e += 64) yi[e] = dyi[e];
+            for (int e = lane; e < N * NET; e += 64) ye[e] = dye[e];
+        }
+        gsync();
+        if (lane == 0) {
+            st.pend = GP_NONE;
+            A.st[b] = st;
+        }
+        return;
+    }
+    const int m = st.mode;
+    auto apply_step = [&](double al, double azz) __attribute__((always_inline)) {
+        for (int e = lane; e < (N + 1) * NX; e += 64) x[e] += al * dx[e];
+        for (int e = lane; e < N * NU; e += 64) u[e] += al * du[e];
+        for (int e = lane; e < N * NIA; e += 64) { s[e] += al * ds[e]; yi[e] += al * dyi[e]; }
+        for (int e = lane; e < N * NX; e += 64) lam[e] += al * dlam[e];
+        for (int e = lane; e < N * NET; e += 64) ye[e] += al * dye[e];
+        if (rsm)
+            for (int r = lane; r < NRI; r += 64)
+                if (el_on(r)) { prr[r] += al * dpr[r]; nrr[r] += al * dnr[r]; }
+        gsync();
+        auto zupd = [&](double &z, double dz, double sl) __attribute__((always_inline)) {
+            const double zz = z + azz * dz;
+            z = fmax(fmin(zz, kappa_sigma * mu / sl), mu / (kappa_sigma * sl));
+        };
+        for (int e = lane + NX; e < (N + 1) * NX; e += 64) {
+            const int j = e % NX;
+            if (gb(P.x_lo[j])) zupd(zxL[e], dzxL[e], x[e] - P.x_lo[j]);
+            if (gb(P.x_hi[j])) zupd(zxU[e], dzxU[e], P.x_hi[j] - x[e]);
+        }
+        for (int e = lane; e < N * NU; e += 64) {
+            if (ufix(e)) continue;
+            if (gb(ulo[e])) zupd(zuL[e], dzuL[e], u[e] - ulo[e]);
+            if (gb(uhi[e])) zupd(zuU[e], dzuU[e], uhi[e] - u[e]);
+        }
+        for (int e = lane; e < N * NI; e += 64) {
+            const int i = (e / NI) * NIA + e % NI;
+            if (gb(clo[e])) zupd(vL[i], dvL[i], s[i] - clo[e]);
+            if (gb(chi[e])) zupd(vU[i], dvU[i], chi[e] - s[i]);
+        }
+        if (rsm)
+            for (int r = lane; r < NRI; r += 64)
+                if (el_on(r)) { zupd(zpr[r], dzp[r], prr[r]); zupd(znr[r], dzn[r], nrr[r]); }
+        gsync();
+    };
+    auto store = [&]() __attribute__((always_inline)) {
+        if (lane == 0) {
+            st.iter++;
+            st.mu = mu;
+            A.st[b] = st;
+        }
+    };
+    double ap, az;
+    ftb(ap, az);
+    double phc, thc, gdc = 0.0;
+    bool okc;
+    merit(x, u, s, true, nullptr, nullptr, nullptr, phc, thc, okc);
+    for (int k = lane; k < N; k += 64) {
+        const double *rk = R(k);
+        for (int a = 0; a < NV; a++) gdc += rk[D::O_GL + a] * (a < NX ? dx[k * NX + a] : du[k * NU + a - NX]);
+    }
+    for (int e = lane; e < N * NU; e += 64) gdc += gu[e] * du[e];
+    for (int e = lane; e < N * NIA; e += 64) gdc += gs[e] * ds[e];
+    for (int e = lane + NX; e < (N + 1) * NX; e += 64) gdc += gx[e] * dx[e];
+    if (rsm)
+        for (int r = lane; r < NRI; r += 64)
+            if (el_on(r)) gdc += (RHO_R + gpr[r]) * dpr[r] + (RHO_R + gnr[r]) * dnr[r];
+    gdc = wave_sum(gdc);
+    if (st.thm[m][0] < 0.0) {
+        st.thm[m][0] = 1e4 * fmax(1.0, thc);
+        st.thm[m][1] = 1e-4 * fmax(1.0, thc);
+    }
+    constexpr double EPS10 = 10.0 * 2.220446049250313e-16;
+    auto ftype = [&](double a, double rth, double rgd) __attribute__((always_inline)) { return rgd < 0.0 && a * pow(-rgd, 2.3) > pow(rth, 1.1); };
+    auto armijo = [&](double a, double ph, double rph, double rgd) __attribute__((always_inline)) { return ph - rph - 1e-8 * a * rgd <= EPS10 * fabs(rph); };
+    // CheckAcceptabilityOfTrialPoint (IpFilterLSAcceptor.cpp); every argument is wave-uniform
+    auto acceptable = [&](double atest, double ph, double th, bool ok, double rph, double rth, double rgd) __attribute__((always_inline)) -> bool {
+        if (!ok || !isfinite(ph) || !isfinite(th)) return false;
+        if (th > st.thm[m][0]) return false;
+        if (atest > 0.0 && ftype(atest, rth, rgd) && rth <= st.thm[m][1]) {
+            if (!armijo(atest, ph, rph, rgd)) return false;
+        } else {
+            if (ph > rph) {
+                const double bas = fabs(rph) > 10.0 ? log10(fabs(rph)) : 1.0;
+                if (log10(ph - rph) > 5.0 + bas) return false;
+            }
+            if (!((th - (1.0 - 1e-5) * rth <= EPS10 * fabs(rth)) || (ph - rph + 1e-8 * rth <= EPS10 * fabs(rph))))
+                return false;
+        }
+        return fil_ok(m, ph, th);
+    };
+    auto alpha_min = [&](double rth, double rgd) __attribute__((always_inline)) {
+        double am = 1e-5;
+        if (rgd < 0.0) {
+            am = fmin(1e-5, 1e-8 * rth / (-rgd));
+            if (rth <= st.thm[m][1]) am = fmin(am, pow(rth, 1.1) / pow(-rgd, 2.3));
+        }
+        return 0.05 * am;
+    };
+    // DoBacktrackingLineSearch with second-order corrections
+    auto backtrack = [&](bool skip_first, bool inwd, double ap_, double th_cur, double rph, double rth, double rgd,
+                         double &alpha_o, double &atest_o, int &ns_o, int &soc_o, double &ph_o, double &azz) __attribute__((always_inline)) -> bool {
+        const double amin = inwd ? ap_ : alpha_min(rth, rgd);
+        double alpha = ap_, atest = inwd ? st.wd_atest : ap_, ph = 0.0, th = 0.0, last = ap_;
+        int ns = 0, soc = 0;
+        bool acc = false;
+        if (skip_first) alpha *= 0.5;
+        while (alpha > amin || ns == 0) {
+            if (!inwd) atest = alpha;
+            last = alpha;
+            trial(alpha);
+            bool ok;
+            merit(tx, tu, ts, false, trdyn, trin, treq, ph, th, ok);
+            if (acceptable(atest, ph, th, ok, rph, rth, rgd)) { acc = true; break; }
+            if (inwd) break;
+            if (ok && alpha == ap_ && th_cur <= th && P.max_soc > 0) {
+                double th_trial = th, th_old = 0.0, a_soc = alpha;
+                for (int e = lane; e < N * NX; e += 64) sdyn[e] = rdyn[e];
+                for (int e = lane; e < N * NIA; e += 64) sin_[e] = rin[e];
+                for (int e = lane; e < N * NET; e += 64) seq[e] = req[e];
+                gsync();
+                for (int cnt = 0; cnt < P.max_soc && (cnt == 0 || th_trial <= 0.99 * th_old); cnt++) {
+                    th_old = th_trial;
+                    for (int e = lane; e < N * NX; e += 64) sdyn[e] = a_soc * sdyn[e] + trdyn[e];
+                    for (int e = lane; e < N * NIA; e += 64) sin_[e] = a_soc * sin_[e] + trin[e];
+                    for (int e = lane; e < N * NET; e += 64) seq[e] = a_soc * seq[e] + treq[e];
+                    gsync();
+                    dir_copy(true);
+                    direction(sdyn, sin_, seq);
+                    double azs;
+                    ftb(a_soc, azs);
+                    trial(a_soc);
+                    bool oks;
+                    merit(tx, tu, ts, false, trdyn, trin, treq, ph, th, oks);
+                    if (acceptable(atest, ph, th, oks, rph, rth, rgd)) {
+                        acc = true; soc = 1; alpha = a_soc; azz = azs;
+                        break;
+                    }
+                    dir_copy(false);
+                    if (!oks) break;
+                    th_trial = th;
+                }
+                if (acc) break;
+            }
+            alpha *= 0.5;
+            ns++;
+        }
+        alpha_o = acc ? alpha : last;
+        atest_o = atest;
+        ns_o = ns;
+        soc_o = soc;
+        ph_o = ph;
+        return acc;
+    };
+    // TrySoftRestoStep (first half): the step min(alpha_primal, alpha_dual) for primal and dual variables;
+    // 1: the original criteria accept it, 2: taken pending the primal-dual error test of the next k_gpre (the
+    // point is kept in wdit), 0: failed
+    auto soft_step = [&](double &a_o) __attribute__((always_inline)) -> int {
+        const double a = fmin(ap, az);
+        a_o = a;
+        trial(a);
+        double ph, th;
+        bool ok;
+        merit(tx, tu, ts, false, nullptr, nullptr, nullptr, ph, th, ok);
+        if (acceptable(0.0, ph, th, ok, phc, thc, gdc)) return 1;
+        if (!ok) return 0;
+        const GErr E = opt_err(mu);
+        st.pd_cur = E.s1 / E.n1;
+        iter_copy_to(A.wdit + b * Z.bk(), true);
+        return 2;
+    };
+    bool want_soft = false, soft_entry = false, go_resto = false, do_step = false;
+    double step_a = 0.0, step_az = 0.0;
+    if (m == 0 && st.in_soft) {  // soft restoration phase: at most max_soft_resto_iters = 10 iterations
+        if (++st.soft_cnt <= 10) want_soft = true;
+        else go_resto = true;
+    } else {
+        if (!st.in_wd && st.wd_short >= 10) {  // StartWatchDog
+            st.in_wd = 1; st.wd_trial = 0; st.n_wd++;
+            st.wd_ph = phc; st.wd_th = thc; st.wd_gd = gdc; st.wd_atest = ap;
+            iter_copy_to(A.wdit + b * Z.bk(), true);
+            dir_copy_to(A.wddir + b * Z.bk(), true);
+        }
+        double rph = st.in_wd ? st.wd_ph : phc, rth = st.in_wd ? st.wd_th : thc, rgd = st.in_wd ? st.wd_gd : gdc;
+        double alpha = ap, atest = ap, pht = 0.0, th_cur = thc;
+        int n_steps = 0, soc_used = 0;
+        bool wd_step = false, accepted = false;
+        for (int pass = 0; pass < 2; pass++) {
+            const bool inwd = pass == 0 && st.in_wd;
+            accepted = backtrack(pass == 1, inwd, ap, th_cur, rph, rth, rgd, alpha, atest, n_steps, soc_used, pht, az);
+            if (!inwd) break;
+            if (accepted) { st.in_wd = 0; break; }
+            if (++st.wd_trial > 3) {  // StopWatchDog: the stored point and direction, backtrack from alpha_max / 2
+                st.in_wd = 0;
+                st.wd_short = 0;
+                iter_copy_to(A.wdit + b * Z.bk(), false);
+                dir_copy_to(A.wddir + b * Z.bk(), false);
+                ftb(ap, az);
+                rph = st.wd_ph; rth = st.wd_th; rgd = st.wd_gd;
+                th_cur = INFINITY;  // (no second-order correction after a skipped first trial point)
+                continue;
+            }
+            accepted = true;  // the watchdog's full trial step, no filter update
+            wd_step = true;
+            alpha = ap;
+            n_steps = 0;
+            break;
+        }
+        if (accepted && !wd_step && (!ftype(atest, rth, rgd) || !armijo(atest, pht, rph, rgd)))
+            fil_add(m, rph - 1e-8 * rth, (1.0 - 1e-5) * rth);
+        if (accepted) {
+            st.n_soc += soc_used;
+            if (!st.in_wd) st.wd_short = (n_steps == 0) ? 0 : st.wd_short + 1;
+            do_step = true;
+            step_a = alpha;
+            step_az = az;
+        } else {
+            st.n_ls_fail++;
+            if (m == 1) { finish(GS_RESTOFAIL); return; }  // no restoration inside the restoration phase
+            // PrepareRestoPhaseStart (the filter takes the current point), then the soft restoration phase, then
+            // the restoration phase if its first step fails
+            fil_add(0, phc - 1e-8 * thc, (1.0 - 1e-5) * thc);
+            ftb(ap, az);
+            want_soft = true;
+            soft_entry = true;
+        }
+    }
+    if (want_soft) {
+        double a = 0.0;
+        const int r = soft_step(a);
+        if (r == 0) {
+            go_resto = true;
+        } else {
+            do_step = true;
+            step_a = step_az = a;
+            if (r == 1) {
+                st.in_soft = 0;
+                st.soft_cnt = 0;
+                st.n_soft++;
+            } else {
+                if (soft_entry) { st.in_soft = 1; st.soft_cnt = 0; }
+                st.pend = GP_SOFT;
+            }
+        }
+    }
+    if (go_resto) {
+        st.rs_ph = phc;
+        st.rs_th = thc;
+        st.in_soft = 0;
+        st.soft_cnt = 0;
+        st.pend = GP_RESTO;
+    }
+    if (do_step) apply_step(step_a, step_az);
+    store();
+    return;
+    }  // flt
     double ap, az;
     ftb(ap, az);
     double phi0, th0;
@@ -1226,7 +1925,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     for (int e = lane; e < N * NX; e += 64) lam[e] += alpha * dlam[e];
     for (int e = lane; e < N * NET; e += 64) ye[e] += alpha * dye[e];
     gsync();
-    auto zupd = [&](double &z, double dz, double sl) {
+    auto zupd = [&](double &z, double dz, double sl) __attribute__((always_inline)) {
         const double zz = z + az * dz;
         z = fmax(fmin(zz, kappa_sigma * mu / sl), mu / (kappa_sigma * sl));
     };
@@ -1258,17 +1957,17 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
 template <class FAM>
 __global__ __launch_bounds__(64) void k_gpre(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
-    giter_phase<FAM, 0>(M0, M1, F0, F1, P, A, batch);
+    giter_phase<FAM, 0, true>(M0, M1, F0, F1, P, A, batch);
 }
 template <class FAM>
 __global__ __launch_bounds__(64) void k_gkkt(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
-    giter_phase<FAM, 1>(M0, M1, F0, F1, P, A, batch);
+    giter_phase<FAM, 1, true>(M0, M1, F0, F1, P, A, batch);
 }
-template <class FAM>
+template <class FAM, bool FLT>
 __global__ __launch_bounds__(64) void k_gls(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                             const DevFrame *F1, GParams P, GArrays A, int batch) {
-    giter_phase<FAM, 2>(M0, M1, F0, F1, P, A, batch);
+    giter_phase<FAM, 2, FLT>(M0, M1, F0, F1, P, A, batch);
 }
 
 // ============================================================== outputs
@@ -1311,7 +2010,7 @@ __global__ __launch_bounds__(256) void k_grec(const DevModel *M0, const DevModel
     const double *x = xu, *u = xu + D::NX;
     if (t < FAM::PRE) FAM::prepass(M, F, P, x, u, t, S);
     __syncthreads();
-    if (t == 0) FAM::seeds(P, u, yi, ye, lam, true, S);
+    if (t == 0) FAM::seeds(P, u, yi, ye, lam, true, 1.0, S);
     __syncthreads();
     if (t < FAM::LANES) FAM::lane(M, F, x, u, yi, t, S);
     __syncthreads();
@@ -1348,6 +2047,9 @@ struct mf_gproblem {
     const DevModel *dM0 = nullptr, *dM1 = nullptr;
     DevFrame *dF0 = nullptr, *dF1 = nullptr;
     double *d_ulo = nullptr, *d_uhi = nullptr, *d_clo = nullptr, *d_chi = nullptr;
+    // the bound tables relaxed by IPOPT's bound_relax_factor (mf_gopts.bound_relax), made on demand
+    double relax = 0.0;
+    double *d_ulo_r = nullptr, *d_uhi_r = nullptr, *d_clo_r = nullptr, *d_chi_r = nullptr;
     int cap = 0;
     int last_batch = 0;  // batch of the last solve (diagnostic reads are bounded by it)
     std::vector<double *> bufs;
@@ -1369,7 +2071,12 @@ template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **
              {&A.trdyn, Z.l()}, {&A.trin, Z.i()}, {&A.treq, Z.e()}, {&A.sdyn, Z.l()}, {&A.sin_, Z.i()},
              {&A.seq, Z.e()},  {&A.tx, Z.x()},   {&A.tu, Z.u()},   {&A.ts, Z.i()},   {&A.P, Z.P()},
              {&A.Kinv, Z.Kinv()}, {&A.Kfb, Z.Kfb()}, {&A.pv, Z.l()}, {&A.kv, Z.kv()}, {&A.x0, (size_t)D::NX},
-             {&A.lref, (size_t)FAM::LREF}, {&A.scr, (size_t)N * scr_words<FAM>()}};
+             {&A.lref, (size_t)FAM::LREF}, {&A.scr, (size_t)N * scr_words<FAM>()},
+             {&A.fil, (size_t)4 * GFCAP}, {&A.wdit, Z.bk()}, {&A.wddir, Z.bk()},
+             {&A.pr, Z.nr()}, {&A.nr, Z.nr()}, {&A.zp, Z.nr()}, {&A.zn, Z.nr()}, {&A.dpr, Z.nr()},
+             {&A.dnr, Z.nr()}, {&A.dzp, Z.nr()}, {&A.dzn, Z.nr()}, {&A.tpr, Z.nr()}, {&A.tnr, Z.nr()},
+             {&A.Sp, Z.nr()}, {&A.Sn, Z.nr()}, {&A.gp, Z.nr()}, {&A.gn, Z.nr()}, {&A.rowr, Z.nr()},
+             {&A.wR, Z.wv()}, {&A.dR, Z.wv()}};
 }
 
 static void gfree_ws(mf_gproblem *p) {
@@ -1428,13 +2135,39 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     P.F_init = o ? o->F_init : 0.0;
     P.max_soc = o ? o->max_soc : 4;
     P.warm_start = (o && d_w0) ? o->warm_start : 0;
+    P.filter = o ? o->filter : 0;
     p->last_batch = batch;
+    // IPOPT bound_relax_factor: every finite bound of a non-fixed variable or row moves out by
+    // br max(1, |b|) (oracle/mf_ocp.c, same rule); fixed controls (lo == hi) stay parameters
+    const double br = o ? o->bound_relax : 0.0;
+    const double *ulo = p->d_ulo, *uhi = p->d_uhi, *clo = p->d_clo, *chi = p->d_chi;
+    if (br != 0.0) {
+        auto lo_r = [&](double v) { return std::isfinite(v) ? v - br * fmax(1.0, fabs(v)) : v; };
+        auto hi_r = [&](double v) { return std::isfinite(v) ? v + br * fmax(1.0, fabs(v)) : v; };
+        for (int j = 0; j < D::NX; j++) { P.x_lo[j] = lo_r(P.x_lo[j]); P.x_hi[j] = hi_r(P.x_hi[j]); }
+        if (br != p->relax || !p->d_ulo_r) {
+            std::vector<double> a(p->ulo), bb(p->uhi), c(p->clo), d(p->chi);
+            for (size_t i = 0; i < a.size(); i++)
+                if (!(std::isfinite(a[i]) && a[i] == bb[i])) { a[i] = lo_r(a[i]); bb[i] = hi_r(bb[i]); }
+            for (size_t i = 0; i < c.size(); i++) { c[i] = lo_r(c[i]); d[i] = hi_r(d[i]); }
+            double **dst[4] = {&p->d_ulo_r, &p->d_uhi_r, &p->d_clo_r, &p->d_chi_r};
+            const std::vector<double> *srcv[4] = {&a, &bb, &c, &d};
+            for (int t = 0; t < 4; t++) {
+                if (!*dst[t]) GHIPCHK(hipMalloc(dst[t], srcv[t]->size() * sizeof(double)));
+                GHIPCHK(hipMemcpyAsync(*dst[t], srcv[t]->data(), srcv[t]->size() * sizeof(double), hipMemcpyHostToDevice, s));
+            }
+            GHIPCHK(hipStreamSynchronize(s));
+            p->relax = br;
+        }
+        ulo = p->d_ulo_r; uhi = p->d_uhi_r; clo = p->d_clo_r; chi = p->d_chi_r;
+    }
     P.has_u_init = (o && o->u_init) ? 1 : 0;
     if (P.has_u_init)
         for (int j = 0; j < D::NU; j++) P.u_init[j] = o->u_init[j];
     GArrays A = p->A;
     A.u0 = d_u0;
     A.w0 = d_w0;
+    A.u_lo = ulo; A.u_hi = uhi; A.c_lo = clo; A.c_hi = chi;
     GHIPCHK(hipMemcpyAsync(A.x0, d_x0, sizeof(double) * D::NX * (size_t)batch, hipMemcpyDeviceToDevice, s));
     if (FAM::LREF != 2) {
         // per-problem data computed by k_ginit from x_0
@@ -1463,7 +2196,8 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             hipLaunchKernelGGL(k_gasm<FAM>, dim3(rec_blocks), dim3(256), 0, s, P, A, batch);
             hipLaunchKernelGGL(k_gpre<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
-            hipLaunchKernelGGL(k_gls<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            if (P.filter) hipLaunchKernelGGL((k_gls<FAM, true>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            else hipLaunchKernelGGL((k_gls<FAM, false>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
         }
         GHIPCHK(hipGetLastError());
         GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1600,7 +2334,7 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
 extern "C" void mf_gproblem_free(mf_gproblem *p) {
     if (!p) return;
     gfree_ws(p);
-    for (double *d : {p->d_ulo, p->d_uhi, p->d_clo, p->d_chi})
+    for (double *d : {p->d_ulo, p->d_uhi, p->d_clo, p->d_chi, p->d_ulo_r, p->d_uhi_r, p->d_clo_r, p->d_chi_r})
         if (d) (void)hipFree(d);
     delete p;
 }

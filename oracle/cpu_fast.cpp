@@ -35,7 +35,7 @@ int record(const Ctx *c, const double *xu, const double *yi, const double *ye, c
     for (int i = 0; i < D::NM; i++) yev[D::NEA + i] = ye[D::NE + i];
     const double *tg = lref;  // line reference (chain) or the 6 pose targets (Centauro)
     for (int t = 0; t < FAM::PRE; t++) FAM::prepass(c->M, c->F, c->P, x, u, t, S);
-    FAM::seeds(c->P, u, yi, yev, lam, eqon != 0, S);
+    FAM::seeds(c->P, u, yi, yev, lam, eqon != 0, 1.0, S);
     for (int t = 0; t < FAM::LANES; t++) FAM::lane(c->M, c->F, x, u, yi, t, S);
     for (int e = 0; e < D::REC; e++) rec[e] = FAM::rec(c->P, x, u, yi, yev, lam, eqon != 0, S, e, tg);
     return D::REC;

@@ -57,7 +57,8 @@ class GOpts(C.Structure):
                 ("w0", C.POINTER(C.c_double)), ("bound_relax", C.c_double),
                 ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("dual_out", C.POINTER(C.c_double)),
                 ("node_cb", C.c_void_p), ("node_ctx", C.c_void_p), ("val_cb", C.c_void_p),
-                ("warm_start", C.c_int), ("dual_in", C.POINTER(C.c_double)), ("riccati", C.c_int)]
+                ("warm_start", C.c_int), ("dual_in", C.POINTER(C.c_double)), ("riccati", C.c_int),
+                ("filter", C.c_int), ("dc_all", C.c_int), ("resto_hard_dyn", C.c_int)]
 
 
 _lib = None
@@ -158,7 +159,7 @@ def make(spec: dict):
         u_lo = np.hstack([np.tile(np.asarray(spec["qd_lo"], float), (N, 1)), np.full((N, 6), -INF)])
         u_hi = np.hstack([np.tile(np.asarray(spec["qd_hi"], float), (N, 1)), np.full((N, 6), INF)])
         u_lo[0, :n] = u_hi[0, :n] = np.asarray(spec["qd0"], float)
-        g.eq_from = 2
+        g.eq_from = int(spec.get("eq_from", 2))
     else:
         m = ms[0]
         n, nf = m.nq, spec["nf"]
@@ -222,9 +223,10 @@ def w_size(g: GOCP) -> int:
 
 def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, verbose=0, F_init=0.0,
          w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None, node_cb=None, node_ctx=None, val_cb=None,
-         warm_start=False, dual_in=None, riccati=False):
+         warm_start=False, dual_in=None, riccati=False, filter=False, dc_all=False, resto_hard_dyn=False):
     o = GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), F_init, None, bound_relax, None,
-              max_soc, None, node_cb, node_ctx, val_cb, int(warm_start), None, int(riccati))
+              max_soc, None, node_cb, node_ctx, val_cb, int(warm_start), None, int(riccati), int(filter), int(dc_all),
+              int(resto_hard_dyn))
     if dual_in is not None:
         o._di = np.ascontiguousarray(dual_in, dtype=np.float64)
         o.dual_in = _p(o._di)

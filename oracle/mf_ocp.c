@@ -121,6 +121,23 @@ typedef struct {
      * [[Q_uu, D_u^T], [D_u, -dc]], Sylvester inertia per stage) instead of the block-tridiagonal
      * Bunch-Kaufman factorisation; the same Newton direction up to round-off (the CPU baseline) */
     int riccati;
+    /* 1: IPOPT's own globalisation instead of the l1-merit search (IpFilterLSAcceptor.cpp and
+     * IpBacktrackingLineSearch.cpp at their defaults): the (theta, phi) filter with the switching
+     * condition, Armijo on the barrier objective for f-type steps, second-order corrections, the filter
+     * reset on every barrier update, the watchdog (10 shortened iterations -> 3 full trial steps), IPOPT's
+     * inertia-correction sequence (IpPDPerturbationHandler.cpp: delta_w = 0 first, 1e-4 / last/3, x100 /
+     * x8), the linear damping kappa_d = 1e-5 of single-bounded variables and mu_min = tol / 11.  Where
+     * IPOPT would enter its restoration phase the iteration takes the shortest trial step instead
+     * (counted in mfg_result.n_ls_fail). */
+    int filter;
+    /* 1: delta_c = 1e-8 mu^(1/4) on every constraint row, the dynamics rows included, from the first
+     * factorisation: IPOPT after it has declared the Jacobian degenerate (the reference transcriptions
+     * keep rows that depend only on the fixed x_0, which makes MUMPS report the KKT singular at every
+     * iteration).  Block-tridiagonal factorisation only. */
+    int dc_all;
+    /* 1: the restoration problem keeps the dynamics rows exact (elastic p, n only on the slack and
+     * equality rows): the variant the device solver's stage-wise Riccati factorisation runs */
+    int resto_hard_dyn;
 } mfg_opts;
 
 typedef struct {
@@ -135,6 +152,7 @@ typedef struct {
 } models_t;
 
 static int hasb(double b) { return isfinite(b); }
+#define KAPPA_D 1e-5  /* IPOPT kappa_d: linear damping of variables with one finite bound (filter mode) */
 
 /* ------------------------------------------------------------------ node functions */
 static void chain_tau(const mfo_model *M, const mfo_frame *Fr, const hd *q, const hd *qd, const hd *Fw, int with_force,
@@ -320,7 +338,21 @@ typedef struct {
     int ric, nk;
     double *Pg, *Kst, *Fg, *pvg, *kvg;
     int *Kpp;
+    /* IPOPT's restoration phase (filter mode, IpRestoIpoptNLP.cpp): the same variables plus elastic
+     * p, n >= 0 on every constraint row, row r in the order [dynamics (N nx) | slack rows (N ni) |
+     * equality rows (N ne)], objective rho sum(p + n) + zeta/2 |D_R (w - w_R)|^2, zeta = sqrt(mu).
+     * p and n are condensed out of the KKT: row r gains the diagonal 1/Sp + 1/Sn and its residual the
+     * term rowr = r_p / Sp - r_n / Sn (the p / n stationarity residuals). */
+    int resto, NR;
+    double objw;                     /* weight of the original objective in node evaluations (0 in resto) */
+    double zeta, rho_r;
+    double *wR, *dR;                 /* reference point and D_R^2 over [x ((N+1) nx) | u (N nu)] */
+    double *pr, *nr, *zp, *zn, *dpr, *dnr, *dzp, *dzn, *tpr, *tnr, *Sp, *Sn, *gp, *gn, *rowr;
 } ws_t;
+
+/* row r of the restoration layout: active, its multiplier */
+static int row_on(const ws_t *S, int r);
+static double *row_y(ws_t *S, int r);
 
 /* per-problem data handed to the node callbacks: the line reference, or the Centauro pose targets
  * (relpos0 and orient0 are adjacent: 6 values) */
@@ -335,6 +367,28 @@ static int vfree(const ws_t *S, int k, int a) {
     if (a < S->nx) return k > 0;
     return !S->ufix[k * S->nu + a - S->nx];
 }
+static int row_on(const ws_t *S, int r) {
+    const int nd = S->N * S->nx, nI = S->N * S->ni;
+    if (r < nd) return 1;
+    if (r < nd + nI) { r -= nd; return CACT(S, r / S->ni, r % S->ni); }
+    r -= nd + nI;
+    return EQ_ON(S, r / S->ne, r % S->ne);
+}
+static double *row_y(ws_t *S, int r) {
+    const int nd = S->N * S->nx, nI = S->N * S->ni;
+    if (r < nd) return S->lam + r;
+    if (r < nd + nI) return S->yi + (r - nd);
+    return S->ye + (r - nd - nI);
+}
+/* row r carries elastic variables in the restoration problem */
+static int row_el(const ws_t *S, int r) {
+    if (S->O->resto_hard_dyn && r < S->N * S->nx) return 0;
+    return row_on(S, r);
+}
+/* resto: extra row diagonal and residual correction of row r (0 outside the restoration phase; Sp = Sn =
+ * inf on rows without elastic variables) */
+#define RDIAG(S, r) ((S)->resto ? 1.0 / (S)->Sp[r] + 1.0 / (S)->Sn[r] : 0.0)
+#define RCORR(S, r) ((S)->resto ? (S)->rowr[r] : 0.0)
 
 static void eval_values(const ws_t *S, int k, const double *x, const double *u, double *l, double *ci, double *ce,
                         double *f) {
@@ -369,6 +423,13 @@ static void eval_derivs(ws_t *S, int k) {
         memcpy(xu + nx, u, nu * sizeof(double));
         S->O->node_cb(S->O->node_ctx, xu, yi, ye, lam, AUX(S->P), eqon, rec);
         (void)REC;
+        if (S->objw != 1.0) {  /* restoration: W without (1 - objw) of the objective's Hessian */
+            double rec0[2 * GV * GV + GV * GI + GX * GX + 512], z[GI + GE + GX];
+            memset(z, 0, sizeof z);
+            S->O->node_cb(S->O->node_ctx, xu, z, z, z, AUX(S->P), eqon, rec0);
+            for (int i = 0; i < nv * nv; i++) rec[oW + i] -= (1.0 - S->objw) * rec0[oW + i];
+            for (int a = 0; a < nv; a++) rec[oGL + a] *= S->objw;
+        }
         S->l[k] = rec[0];
         memcpy(gl, rec + oGL, nv * sizeof(double));
         memcpy(S->ci + k * ni, rec + oCI, ni * sizeof(double));
@@ -415,14 +476,14 @@ static void eval_derivs(ws_t *S, int k) {
             hx[a].b = 1.0;
             hx[b].c = 1.0;
             node_hd(S->P, S->MM, hx, &hl, hci, hce, hf);
-            double h2 = hl.d;
+            double h2 = S->objw * hl.d;
             for (int r = 0; r < ni; r++) h2 += yi[r] * hci[r].d;
             for (int e = 0; e < ne; e++)
                 if (EQ_ON(S, k, e)) h2 += ye[e] * hce[e].d;
             for (int j = 0; j < nx; j++) h2 += lam[j] * hf[j].d;
             W[a * nv + b] = W[b * nv + a] = h2;
             if (a == b) {
-                gl[a] = hl.b;
+                gl[a] = S->objw * hl.b;
                 for (int r = 0; r < ni; r++) Ji[r * nv + a] = hci[r].b;
                 for (int e = 0; e < ne; e++) Je[e * nv + a] = hce[e].b;
                 if (a < nx) {
@@ -451,39 +512,69 @@ static double push_into_k(double x, double lo, double hi, double k1, double k2) 
 }
 static double push_into(double x, double lo, double hi) { return push_into_k(x, lo, hi, 1e-2, 1e-2); }
 
-/* barrier objective and l1 constraint violation at (x, u, s); optionally the residual vectors */
-static void merit_parts(const ws_t *S, const double *x, const double *u, const double *s, double mu, double *phi,
-                        double *theta, int *ok, double *rdyn, double *rin, double *req) {
+/* barrier objective and l1 constraint violation at (x, u, s); optionally the residual vectors.
+ * pp, nn: the restoration problem's elastic variables at this point (NULL: the original problem). */
+#define merit_parts(S, x, u, s, mu, phi, theta, ok, rdyn, rin, req) \
+    merit_parts_e(S, x, u, s, NULL, NULL, mu, phi, theta, ok, rdyn, rin, req)
+static void merit_parts_e(const ws_t *S, const double *x, const double *u, const double *s, const double *pp,
+                          const double *nn, double mu, double *phi, double *theta, int *ok, double *rdyn, double *rin,
+                          double *req) {
     const int N = S->N, nx = S->nx, nu = S->nu, ni = S->ni, ne = S->ne;
+    const int oI = N * nx, oE = N * nx + N * ni;
     double fsum = 0, bar = 0, th = 0;
     int good = 1;
+#define EL(r) (pp ? nn[r] - pp[r] : 0.0)
 #ifdef _OPENMP
 #pragma omp parallel for reduction(+ : fsum, th) schedule(static)
 #endif
     for (int k = 0; k < N; k++) {
         double l, ci[GI], ce[GE], f[GX];
         eval_values(S, k, x + k * nx, u + k * nu, &l, ci, ce, f);
-        fsum += l;
+        if (!pp) fsum += l;
         for (int j = 0; j < nx; j++) {
-            const double r = f[j] - x[(k + 1) * nx + j];
+            const double r = f[j] - x[(k + 1) * nx + j] + EL(k * nx + j);
             th += fabs(r);
             if (rdyn) rdyn[k * nx + j] = r;
         }
         for (int q = 0; q < ni; q++) {
-            const double r = CACT(S, k, q) ? ci[q] - s[k * ni + q] : 0.0;
+            const double r = CACT(S, k, q) ? ci[q] - s[k * ni + q] + EL(oI + k * ni + q) : 0.0;
             th += fabs(r);
             if (rin) rin[k * ni + q] = r;
         }
         for (int e = 0; e < ne; e++) {
-            const double r = EQ_ON(S, k, e) ? ce[e] : 0.0;
+            const double r = EQ_ON(S, k, e) ? ce[e] + EL(oE + k * ne + e) : 0.0;
             th += fabs(r);
             if (req) req[k * ne + e] = r;
         }
     }
+#undef EL
+    if (pp) {  /* restoration objective: rho sum(p + n) + zeta/2 |D_R (w - w_R)|^2, barrier on p, n */
+        double pn = 0, prox = 0, lbar = 0;
+        for (int r = 0; r < S->NR; r++)
+            if (row_el(S, r)) {
+                pn += pp[r] + nn[r];
+                if (pp[r] <= 0 || nn[r] <= 0) good = 0;
+                else lbar -= log(pp[r]) + log(nn[r]);
+            }
+        for (int k = 1; k <= N; k++)
+            for (int j = 0; j < nx; j++) {
+                const int i = k * nx + j;
+                prox += S->dR[i] * (x[i] - S->wR[i]) * (x[i] - S->wR[i]);
+            }
+        for (int i = 0; i < N * nu; i++)
+            if (!S->ufix[i]) {
+                const int o = (N + 1) * nx + i;
+                prox += S->dR[o] * (u[i] - S->wR[o]) * (u[i] - S->wR[o]);
+            }
+        fsum = S->rho_r * pn + 0.5 * S->zeta * prox + mu * lbar + KAPPA_D * mu * pn;
+    }
+    double lin = 0;  /* IPOPT kappa_d damping of single-bounded variables (filter mode) */
 #define BAR(v, lo, hi)                                              \
     do {                                                            \
         if (hasb(lo)) { if ((v) - (lo) <= 0) good = 0; else bar -= log((v) - (lo)); } \
         if (hasb(hi)) { if ((hi) - (v) <= 0) good = 0; else bar -= log((hi) - (v)); } \
+        if (hasb(lo) && !hasb(hi)) lin += (v) - (lo);               \
+        if (hasb(hi) && !hasb(lo)) lin += (hi) - (v);               \
     } while (0)
     for (int k = 1; k <= N; k++)
         for (int j = 0; j < nx; j++) BAR(x[k * nx + j], S->xlo[j], S->xhi[j]);
@@ -493,7 +584,7 @@ static void merit_parts(const ws_t *S, const double *x, const double *u, const d
     for (int k = 0; k < N; k++)
         for (int r = 0; r < ni; r++) BAR(s[k * ni + r], S->clo[k * ni + r], S->chi[k * ni + r]);
 #undef BAR
-    *phi = fsum + mu * bar;
+    *phi = fsum + mu * bar + (S->O->filter ? KAPPA_D * mu * lin : 0.0);
     *theta = th;
     *ok = good;
 }
@@ -504,6 +595,16 @@ static void residuals_cached(const ws_t *S, double *rdyn, double *rin, double *r
         for (int j = 0; j < nx; j++) rdyn[k * nx + j] = S->f[k * nx + j] - S->x[(k + 1) * nx + j];
         for (int q = 0; q < ni; q++) rin[k * ni + q] = CACT(S, k, q) ? S->ci[k * ni + q] - S->s[k * ni + q] : 0.0;
         for (int e = 0; e < ne; e++) req[k * ne + e] = EQ_ON(S, k, e) ? S->ce[k * ne + e] : 0.0;
+    }
+    if (S->resto) {  /* the restoration rows g - p + n */
+        const int oI = N * nx, oE = N * nx + N * ni;
+        for (int r = 0; r < S->NR; r++) {
+            if (!row_el(S, r)) continue;
+            const double el = S->nr[r] - S->pr[r];
+            if (r < oI) rdyn[r] += el;
+            else if (r < oE) rin[r - oI] += el;
+            else req[r - oE] += el;
+        }
     }
 }
 
@@ -524,8 +625,9 @@ static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
         memset(Dm, 0, sizeof(double) * mb * mb);
 #define D_(i, j) Dm[(i) * m + (j)]
         for (int j = 0; j < nx; j++) {
-            if (k > 0) {  /* dynamics rows stay unregularised (delta_c acts on c_eq and slack rows) */
+            if (k > 0) {  /* dynamics rows stay unregularised unless dc_all (delta_c acts on c_eq and slack rows) */
                 D_(ol + j, ox + j) = D_(ox + j, ol + j) = -1.0;
+                if (S->O->dc_all || S->resto) D_(ol + j, ol + j) = -(S->O->dc_all ? dc : 0.0) - RDIAG(S, (k - 1) * nx + j);
             } else {
                 D_(ol + j, ol + j) = -1.0; /* lam_{-1}: dummy */
             }
@@ -536,7 +638,7 @@ static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
             double Dd[GI];
             for (int q = 0; q < ni; q++) {
                 const double sg = S->Ss[k * ni + q] + dw;
-                Dd[q] = CACT(S, k, q) ? sg / (1.0 + dc * sg) : 0.0;
+                Dd[q] = CACT(S, k, q) ? sg / (1.0 + (dc + RDIAG(S, N * nx + k * ni + q)) * sg) : 0.0;
             }
             for (int a = 0; a < nv; a++)
                 for (int b = 0; b < nv; b++) {
@@ -556,7 +658,7 @@ static int kkt_factor(ws_t *S, double dw, double dc, double d1) {
             for (int e = 0; e < ne; e++) {
                 if (EQ_ON(S, k, e)) {
                     for (int j = 0; j < nv; j++) D_(oe + e, ox + j) = D_(ox + j, oe + e) = Je[e * nv + j];
-                    D_(oe + e, oe + e) = -dc;
+                    D_(oe + e, oe + e) = -dc - RDIAG(S, N * nx + N * ni + k * ne + e);
                 } else {
                     D_(oe + e, oe + e) = -1.0;
                 }
@@ -618,9 +720,10 @@ static void slack_and_bound_steps(ws_t *S, double mu, const double *rin) {
             double jd = 0;
             for (int a = 0; a < nx; a++) jd += Ji[q * nv + a] * S->dx[k * nx + a];
             for (int a = 0; a < nu; a++) jd += Ji[q * nv + nx + a] * S->du[k * nu + a];
-            const double sg = S->Ss[i] + dw, Dd = sg / (1.0 + dc * sg);
+            const int rr = N * nx + i;
+            const double sg = S->Ss[i] + dw, Dd = sg / (1.0 + (dc + RDIAG(S, rr)) * sg);
             const double rs = S->gs[i] - S->yi[i];
-            S->dyi[i] = Dd * (jd + rin[i] + rs / sg);
+            S->dyi[i] = Dd * (jd + rin[i] + RCORR(S, rr) + rs / sg);
             S->ds[i] = (S->dyi[i] - rs) / sg;
         }
     }
@@ -643,6 +746,18 @@ static void slack_and_bound_steps(ws_t *S, double mu, const double *rin) {
     for (int i = 0; i < N * ni; i++)
         DZ(S->dvL[i], S->dvU[i], S->vL[i], S->vU[i], S->s[i], S->ds[i], S->clo[i], S->chi[i]);
 #undef DZ
+    if (S->resto) /* the elastic variables: Sp dp = dy - r_p, Sn dn = -dy - r_n, and their bound multipliers */
+        for (int r = 0; r < S->NR; r++) {
+            if (!row_el(S, r)) { S->dpr[r] = S->dnr[r] = S->dzp[r] = S->dzn[r] = 0.0; continue; }
+            const int nd = N * nx, nI = N * ni;
+            const double dy = r < nd ? S->dlam[r] : (r < nd + nI ? S->dyi[r - nd] : S->dye[r - nd - nI]);
+            const double y = *row_y(S, r);
+            const double rp = S->rho_r + S->gp[r] - y, rn = S->rho_r + S->gn[r] + y;
+            S->dpr[r] = (dy - rp) / S->Sp[r];
+            S->dnr[r] = (-dy - rn) / S->Sn[r];
+            S->dzp[r] = mu / S->pr[r] - S->zp[r] - S->zp[r] / S->pr[r] * S->dpr[r];
+            S->dzn[r] = mu / S->nr[r] - S->zn[r] - S->zn[r] / S->nr[r] * S->dnr[r];
+        }
 }
 
 /* Newton direction with the stored factorisation for constraint residuals (rdyn, rin, req): the
@@ -656,7 +771,7 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
         double *r = S->wv + (size_t)k * mb;
         memset(r, 0, sizeof(double) * mb);
         if (k > 0)
-            for (int j = 0; j < nx; j++) r[ol + j] = -rdyn[(k - 1) * nx + j];
+            for (int j = 0; j < nx; j++) r[ol + j] = -(rdyn[(k - 1) * nx + j] + RCORR(S, (k - 1) * nx + j));
         if (k < N) {
             const double *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + (size_t)k * ne * nv;
             double Dd[GI], rdd[GI];
@@ -664,11 +779,12 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
                 const int i = k * ni + q;
                 if (CACT(S, k, q)) {
                     const double sg = S->Ss[i] + dw;
-                    Dd[q] = sg / (1.0 + dc * sg);
-                    rdd[q] = rin[i] + (S->gs[i] - S->yi[i]) / sg;
+                    Dd[q] = sg / (1.0 + (dc + RDIAG(S, N * nx + i)) * sg);
+                    rdd[q] = rin[i] + RCORR(S, N * nx + i) + (S->gs[i] - S->yi[i]) / sg;
                 } else { Dd[q] = 0; rdd[q] = 0; }
             }
-            for (int e = 0; e < ne; e++) r[oe + e] = EQ_ON(S, k, e) ? -req[k * ne + e] : 0.0;
+            for (int e = 0; e < ne; e++)
+                r[oe + e] = EQ_ON(S, k, e) ? -(req[k * ne + e] + RCORR(S, N * nx + N * ni + k * ne + e)) : 0.0;
             for (int a = 0; a < nv; a++) {
                 if (!vfree(S, k, a)) { r[ox + a] = 0; continue; }
                 double g = S->gl[k * nv + a];
@@ -983,6 +1099,12 @@ static void ftb(const ws_t *S, double tau_fb, double *ap_out, double *az_out) {
         if (!S->ufix[i]) FTB(S->u[i], S->du[i], S->ulo[i], S->uhi[i], S->zuL[i], S->dzuL[i], S->zuU[i], S->dzuU[i]);
     for (int i = 0; i < N * ni; i++)
         FTB(S->s[i], S->ds[i], S->clo[i], S->chi[i], S->vL[i], S->dvL[i], S->vU[i], S->dvU[i]);
+    if (S->resto)
+        for (int r = 0; r < S->NR; r++)
+            if (row_el(S, r)) {
+                FTB(S->pr[r], S->dpr[r], 0.0, INFINITY, S->zp[r], S->dzp[r], 0.0, 0.0);
+                FTB(S->nr[r], S->dnr[r], 0.0, INFINITY, S->zn[r], S->dzn[r], 0.0, 0.0);
+            }
     *ap_out = ap;
     *az_out = az;
 }
@@ -1036,6 +1158,9 @@ static void direction_model(const ws_t *S, double *gdot_out, double *pHp_out) {
         gdot += S->gx[i] * S->dx[i];
         pHp += S->Sx[i] * S->dx[i] * S->dx[i];
     }
+    if (S->resto)
+        for (int r = 0; r < S->NR; r++)
+            if (row_el(S, r)) gdot += (S->rho_r + S->gp[r]) * S->dpr[r] + (S->rho_r + S->gn[r]) * S->dnr[r];
     *gdot_out = gdot;
     *pHp_out = pHp;
 }
@@ -1045,6 +1170,11 @@ static void trial_point(ws_t *S, double alpha) {
     for (size_t i = 0; i < NX1; i++) S->tx[i] = S->x[i] + alpha * S->dx[i];
     for (size_t i = 0; i < NU; i++) S->tu[i] = S->u[i] + alpha * S->du[i];
     for (size_t i = 0; i < NI; i++) S->ts[i] = S->s[i] + alpha * S->ds[i];
+    if (S->resto)
+        for (int r = 0; r < S->NR; r++) {
+            S->tpr[r] = S->pr[r] + alpha * S->dpr[r];
+            S->tnr[r] = S->nr[r] + alpha * S->dnr[r];
+        }
 }
 
 /* the direction arrays, in a fixed order, for save / restore around second-order corrections */
@@ -1052,22 +1182,164 @@ static int dir_arrays(ws_t *S, double ***arr, size_t *len) {
     const size_t NX1 = (size_t)(S->N + 1) * S->nx, NXN = (size_t)S->N * S->nx, NU = (size_t)S->N * S->nu,
                  NI = (size_t)S->N * S->ni, NE = (size_t)S->N * S->ne;
     double **a[] = {&S->dx, &S->du, &S->ds, &S->dlam, &S->dye, &S->dyi, &S->dzxL, &S->dzxU, &S->dzuL, &S->dzuU,
-                    &S->dvL, &S->dvU};
-    const size_t l[] = {NX1, NU, NI, NXN, NE, NI, NX1, NX1, NU, NU, NI, NI};
-    for (int i = 0; i < 12; i++) { arr[i] = a[i]; len[i] = l[i]; }
-    return 12;
+                    &S->dvL, &S->dvU, &S->dpr, &S->dnr, &S->dzp, &S->dzn};
+    const size_t l[] = {NX1, NU, NI, NXN, NE, NI, NX1, NX1, NU, NU, NI, NI, S->NR, S->NR, S->NR, S->NR};
+    for (int i = 0; i < 16; i++) { arr[i] = a[i]; len[i] = l[i]; }
+    return S->resto ? 16 : 12;
 }
 static void save_direction(ws_t *S) {
-    double **arr[12];
-    size_t len[12], off = 0;
+    double **arr[16];
+    size_t len[16], off = 0;
     const int na = dir_arrays(S, arr, len);
     for (int i = 0; i < na; i++) { memcpy(S->bk + off, *arr[i], len[i] * sizeof(double)); off += len[i]; }
 }
 static void restore_direction(ws_t *S) {
-    double **arr[12];
-    size_t len[12], off = 0;
+    double **arr[16];
+    size_t len[16], off = 0;
     const int na = dir_arrays(S, arr, len);
     for (int i = 0; i < na; i++) { memcpy(*arr[i], S->bk + off, len[i] * sizeof(double)); off += len[i]; }
+}
+
+/* the iterate arrays, in a fixed order, for the watchdog's stored point */
+static int iter_arrays(ws_t *S, double ***arr, size_t *len) {
+    const size_t NX1 = (size_t)(S->N + 1) * S->nx, NXN = (size_t)S->N * S->nx, NU = (size_t)S->N * S->nu,
+                 NI = (size_t)S->N * S->ni, NE = (size_t)S->N * S->ne;
+    double **a[] = {&S->x, &S->u, &S->s, &S->lam, &S->ye, &S->yi, &S->zxL, &S->zxU, &S->zuL, &S->zuU, &S->vL, &S->vU,
+                    &S->pr, &S->nr, &S->zp, &S->zn};
+    const size_t l[] = {NX1, NU, NI, NXN, NE, NI, NX1, NX1, NU, NU, NI, NI, S->NR, S->NR, S->NR, S->NR};
+    for (int i = 0; i < 16; i++) { arr[i] = a[i]; len[i] = l[i]; }
+    return S->resto ? 16 : 12;
+}
+static void copy_arrays(ws_t *S, int (*fn)(ws_t *, double ***, size_t *), double *buf, int to_buf) {
+    double **arr[16];
+    size_t len[16], off = 0;
+    const int na = fn(S, arr, len);
+    for (int i = 0; i < na; i++) {
+        if (to_buf) memcpy(buf + off, *arr[i], len[i] * sizeof(double));
+        else memcpy(*arr[i], buf + off, len[i] * sizeof(double));
+        off += len[i];
+    }
+}
+
+/* ---- IPOPT's filter line search (mfg_opts.filter) ----
+ * Constants are IPOPT's defaults (IpFilterLSAcceptor.cpp): gamma_theta 1e-5, gamma_phi 1e-8, delta 1,
+ * s_theta 1.1, s_phi 2.3, eta_phi 1e-8, theta_max = 1e4 max(1, theta_0), theta_min = 1e-4 max(1, theta_0),
+ * alpha_min_frac 0.05, kappa_soc 0.99, obj_max_inc 5.  theta is the l1 norm of (c, d - s), phi the
+ * barrier objective. */
+typedef struct {
+    double *fph, *fth;  /* filter entries (phi, theta), already margined */
+    int nf, cap;
+    double theta_max, theta_min;
+    double rph, rth, rgd;  /* reference point: phi, theta, grad phi^T d */
+} filt_t;
+
+static int ls_le(double a, double b, double bas) { return a - b <= 10.0 * 2.220446049250313e-16 * fabs(bas); }
+static int ls_ftype(const filt_t *L, double a) {
+    return L->rgd < 0.0 && a * pow(-L->rgd, 2.3) > pow(L->rth, 1.1);
+}
+static int ls_armijo(const filt_t *L, double a, double ph) { return ls_le(ph - L->rph, 1e-8 * a * L->rgd, L->rph); }
+static int ls_acceptable(const filt_t *L, double atest, double ph, double th, int ok) {
+    if (!ok || !isfinite(ph) || !isfinite(th)) return 0;
+    if (th > L->theta_max) return 0;
+    if (atest > 0.0 && ls_ftype(L, atest) && L->rth <= L->theta_min) {
+        if (!ls_armijo(L, atest, ph)) return 0;
+    } else {
+        if (ph > L->rph) {
+            const double bas = fabs(L->rph) > 10.0 ? log10(fabs(L->rph)) : 1.0;
+            if (log10(ph - L->rph) > 5.0 + bas) return 0;
+        }
+        if (!(ls_le(th, (1.0 - 1e-5) * L->rth, L->rth) || ls_le(ph - L->rph, -1e-8 * L->rth, L->rph))) return 0;
+    }
+    for (int j = 0; j < L->nf; j++)
+        if (!(ph <= L->fph[j] || th <= L->fth[j])) return 0;
+    return 1;
+}
+static void ls_augment(filt_t *L) {
+    if (L->nf == L->cap) {
+        L->cap = L->cap ? 2 * L->cap : 64;
+        L->fph = (double *)realloc(L->fph, L->cap * sizeof(double));
+        L->fth = (double *)realloc(L->fth, L->cap * sizeof(double));
+    }
+    L->fph[L->nf] = L->rph - 1e-8 * L->rth;
+    L->fth[L->nf] = (1.0 - 1e-5) * L->rth;
+    L->nf++;
+}
+static double ls_alpha_min(const filt_t *L) {
+    double am = 1e-5;
+    if (L->rgd < 0.0) {
+        am = fmin(1e-5, 1e-8 * L->rth / (-L->rgd));
+        if (L->rth <= L->theta_min) am = fmin(am, pow(L->rth, 1.1) / pow(-L->rgd, 2.3));
+    }
+    return 0.05 * am;
+}
+
+#define TP(S) ((S)->resto ? (S)->tpr : NULL)
+#define TN(S) ((S)->resto ? (S)->tnr : NULL)
+/* DoBacktrackingLineSearch (IpBacktrackingLineSearch.cpp): trial steps alpha_max, alpha_max/2, ... down to
+ * alpha_min; a second-order correction after a rejected first trial point that did not lower theta below
+ * the current one (thc); in the watchdog only the full step is tried, tested with the watchdog's alpha.
+ * Returns 1 with the accepted step (alpha, az, and the SOC direction left in place when one was taken). */
+static int filter_backtrack(ws_t *S, const filt_t *L, double mu, double tau_fb, double ap, double thc, int skip_first,
+                            int in_wd, double wd_atest, double *alpha_out, double *az_io, double *atest_out,
+                            int *nsteps_out, int *soc_out, double *ph_out, double *th_out, double *ts) {
+    const int N = S->N, nx = S->nx, ni = S->ni, ne = S->ne;
+    const double alpha_min = in_wd ? ap : ls_alpha_min(L);
+    double alpha = ap, atest = in_wd ? wd_atest : ap, ph = 0, th = 0, t_ph, last = ap;
+    int n_steps = 0, accept = 0, soc = 0, ok;
+    if (skip_first) alpha *= 0.5;
+    while (alpha > alpha_min || n_steps == 0) {
+        if (!in_wd) atest = alpha;
+        last = alpha;
+        trial_point(S, alpha);
+        t_ph = wall_s();
+        merit_parts_e(S, S->tx, S->tu, S->ts, TP(S), TN(S), mu, &ph, &th, &ok, S->trdyn, S->trin, S->treq);
+        ts[3] += wall_s() - t_ph;
+        if (ls_acceptable(L, atest, ph, th, ok)) { accept = 1; break; }
+        if (in_wd) break;
+        if (ok && alpha == ap && thc <= th && S->O->max_soc > 0) {
+            double th_trial = th, th_old = 0.0, a_soc = alpha;
+            for (size_t i = 0; i < (size_t)N * nx; i++) S->sdyn[i] = S->rdyn[i];
+            for (size_t i = 0; i < (size_t)N * ni; i++) S->sin_[i] = S->rin[i];
+            for (size_t i = 0; i < (size_t)N * ne; i++) S->seq[i] = S->req[i];
+            for (int cnt = 0; cnt < S->O->max_soc && (cnt == 0 || th_trial <= 0.99 * th_old); cnt++) {
+                th_old = th_trial;
+                for (size_t i = 0; i < (size_t)N * nx; i++) S->sdyn[i] = a_soc * S->sdyn[i] + S->trdyn[i];
+                for (size_t i = 0; i < (size_t)N * ni; i++) S->sin_[i] = a_soc * S->sin_[i] + S->trin[i];
+                for (size_t i = 0; i < (size_t)N * ne; i++) S->seq[i] = a_soc * S->seq[i] + S->treq[i];
+                save_direction(S);
+                t_ph = wall_s();
+                (S->ric ? kkt_direction_ric : kkt_direction)(S, mu, S->sdyn, S->sin_, S->seq);
+                ts[2] += wall_s() - t_ph;
+                double azs;
+                ftb(S, tau_fb, &a_soc, &azs);
+                trial_point(S, a_soc);
+                int oks;
+                t_ph = wall_s();
+                merit_parts_e(S, S->tx, S->tu, S->ts, TP(S), TN(S), mu, &ph, &th, &oks, S->trdyn, S->trin, S->treq);
+                ts[3] += wall_s() - t_ph;
+                if (S->O->verbose > 1)
+                    fprintf(stderr, "      soc %d a %.3e th %.3e (ref %.3e) phi %.10e (ref %.10e)\n", cnt, a_soc, th,
+                            L->rth, ph, L->rph);
+                if (ls_acceptable(L, atest, ph, th, oks)) {
+                    accept = 1; soc = 1; alpha = a_soc; *az_io = azs;
+                    break;
+                }
+                restore_direction(S);
+                if (!oks) break;
+                th_trial = th;
+            }
+            if (accept) break;
+        }
+        alpha *= 0.5;
+        n_steps++;
+    }
+    *alpha_out = accept ? alpha : last;  /* rejected: the last (shortest) trial step */
+    *atest_out = atest;
+    *nsteps_out = n_steps;
+    *soc_out = soc;
+    *ph_out = ph;
+    *th_out = th;
+    return accept;
 }
 
 /* relative-pose targets of the Centauro rows from x_0: RelativePosition / RelativeOrientationError at
@@ -1084,6 +1356,560 @@ static void cent_targets(mfg_ocp *P, const models_t *MM) {
         P->relpos0[b] = hce[b].a;
         P->orient0[b] = sc > 0 ? rint(hce[3 + b].a * sc) / sc : hce[3 + b].a;
     }
+}
+
+
+/* ==================================================================== IPOPT mode (mfg_opts.filter) ==== */
+/* optimality measures at the current point (its derivatives evaluated): IPOPT's scaled E_0 pieces (max
+ * norms) and the primal-dual system error of the soft restoration phase (1-norms / count).  In the
+ * restoration phase they are those of the restoration problem. */
+typedef struct {
+    double dinf, pinf, cinf0, cinfm, sd, sc;
+    double s1, n1;  /* sum of |dual inf| + |primal inf| + |z gap - mu|, and the number of terms */
+} errs_t;
+
+static void opt_error_f(const ws_t *S, double mu, errs_t *E) {
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne;
+    const double s_max = 100.0;
+    double dinf = 0, pinf = 0, cinf0 = 0, cinfm = 0, sum_mult = 0, sum_bmult = 0, s1 = 0, n1 = 0;
+    int n_mult = 0, n_bmult = 0;
+#define COMPF(z, gap)                                                                           \
+    do {                                                                                        \
+        double c_ = (z) * (gap);                                                                \
+        cinf0 = fmax(cinf0, fabs(c_)); cinfm = fmax(cinfm, fabs(c_ - mu));                      \
+        sum_bmult += (z); n_bmult++; s1 += fabs(c_ - mu); n1 += 1;                              \
+    } while (0)
+#define DUALF(r) do { dinf = fmax(dinf, fabs(r)); s1 += fabs(r); n1 += 1; } while (0)
+#define PRIMF(r) do { pinf = fmax(pinf, fabs(r)); s1 += fabs(r); n1 += 1; } while (0)
+    for (int k = 1; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            double r = -S->lam[(k - 1) * nx + j];
+            if (k < N) {
+                r += S->gl[k * nv + j];
+                for (int jj = 0; jj < nx; jj++) r += S->Af[(k * nx + jj) * nx + j] * S->lam[k * nx + jj];
+                for (int q = 0; q < ni; q++) r += S->Ji[((size_t)k * ni + q) * nv + j] * S->yi[k * ni + q];
+                for (int e = 0; e < ne; e++)
+                    if (EQ_ON(S, k, e)) r += S->Je[((size_t)k * ne + e) * nv + j] * S->ye[k * ne + e];
+            }
+            if (S->resto) r += S->zeta * S->dR[i] * (S->x[i] - S->wR[i]);
+            r += -S->zxL[i] + S->zxU[i];
+            DUALF(r);
+            if (hasb(S->xlo[j])) COMPF(S->zxL[i], S->x[i] - S->xlo[j]);
+            if (hasb(S->xhi[j])) COMPF(S->zxU[i], S->xhi[j] - S->x[i]);
+        }
+    for (int k = 0; k < N; k++) {
+        for (int j = 0; j < nu; j++) {
+            const int i = k * nu + j;
+            if (S->ufix[i]) continue;
+            double r = S->gl[k * nv + nx + j];
+            for (int jj = 0; jj < nx; jj++) r += S->Bf[(k * nx + jj) * nu + j] * S->lam[k * nx + jj];
+            for (int q = 0; q < ni; q++) r += S->Ji[((size_t)k * ni + q) * nv + nx + j] * S->yi[k * ni + q];
+            for (int e = S->nes; e < ne; e++) r += S->Je[((size_t)k * ne + e) * nv + nx + j] * S->ye[k * ne + e];
+            if (S->resto) {
+                const int o = (N + 1) * nx + i;
+                r += S->zeta * S->dR[o] * (S->u[i] - S->wR[o]);
+            }
+            r += -S->zuL[i] + S->zuU[i];
+            DUALF(r);
+            if (hasb(S->ulo[i])) COMPF(S->zuL[i], S->u[i] - S->ulo[i]);
+            if (hasb(S->uhi[i])) COMPF(S->zuU[i], S->uhi[i] - S->u[i]);
+        }
+        for (int q = 0; q < ni; q++) {
+            const int i = k * ni + q;
+            if (!CACT(S, k, q)) continue;
+            double r = -S->yi[i] - S->vL[i] + S->vU[i];
+            DUALF(r);
+            if (hasb(S->clo[i])) COMPF(S->vL[i], S->s[i] - S->clo[i]);
+            if (hasb(S->chi[i])) COMPF(S->vU[i], S->chi[i] - S->s[i]);
+            PRIMF(S->rin[i]);
+            sum_mult += fabs(S->yi[i]); n_mult++;
+        }
+        for (int j = 0; j < nx; j++) {
+            PRIMF(S->rdyn[k * nx + j]);
+            sum_mult += fabs(S->lam[k * nx + j]); n_mult++;
+        }
+        for (int e = 0; e < ne; e++)
+            if (EQ_ON(S, k, e)) {
+                PRIMF(S->req[k * ne + e]);
+                sum_mult += fabs(S->ye[k * ne + e]); n_mult++;
+            }
+    }
+    if (S->resto)
+        for (int r = 0; r < S->NR; r++) {
+            if (!row_el(S, r)) continue;
+            const double y = *row_y((ws_t *)S, r);
+            DUALF(S->rho_r - y - S->zp[r]);
+            DUALF(S->rho_r + y - S->zn[r]);
+            COMPF(S->zp[r], S->pr[r]);
+            COMPF(S->zn[r], S->nr[r]);
+        }
+#undef COMPF
+#undef DUALF
+#undef PRIMF
+    E->dinf = dinf; E->pinf = pinf; E->cinf0 = cinf0; E->cinfm = cinfm;
+    E->sd = fmax(s_max, (sum_mult + sum_bmult) / fmax(1, n_mult + n_bmult)) / s_max;
+    E->sc = fmax(s_max, sum_bmult / fmax(1, n_bmult)) / s_max;
+    E->s1 = s1; E->n1 = n1;
+}
+
+/* Sigma, barrier gradients (with kappa_d) and, in the restoration phase, the proximity term (folded into
+ * Sigma / gradient of x, u) and the condensed elastic rows */
+static void barrier_f(ws_t *S, double mu) {
+    const int N = S->N, nx = S->nx, nu = S->nu;
+#define SIGF(Sg, gg, z_l, z_u, v, lo, hi)                                                   \
+    do {                                                                                   \
+        Sg = 0; gg = 0;                                                                    \
+        if (hasb(lo)) { Sg += (z_l) / ((v) - (lo)); gg -= mu / ((v) - (lo)); }             \
+        if (hasb(hi)) { Sg += (z_u) / ((hi) - (v)); gg += mu / ((hi) - (v)); }             \
+        if (hasb(lo) && !hasb(hi)) gg += KAPPA_D * mu;                                     \
+        if (hasb(hi) && !hasb(lo)) gg -= KAPPA_D * mu;                                     \
+    } while (0)
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            if (k == 0) { S->Sx[i] = S->gx[i] = 0; continue; }
+            SIGF(S->Sx[i], S->gx[i], S->zxL[i], S->zxU[i], S->x[i], S->xlo[j], S->xhi[j]);
+            if (S->resto) { S->Sx[i] += S->zeta * S->dR[i]; S->gx[i] += S->zeta * S->dR[i] * (S->x[i] - S->wR[i]); }
+        }
+    for (int i = 0; i < N * nu; i++) {
+        if (S->ufix[i]) { S->Su[i] = S->gu[i] = 0; continue; }
+        SIGF(S->Su[i], S->gu[i], S->zuL[i], S->zuU[i], S->u[i], S->ulo[i], S->uhi[i]);
+        if (S->resto) {
+            const int o = (N + 1) * nx + i;
+            S->Su[i] += S->zeta * S->dR[o];
+            S->gu[i] += S->zeta * S->dR[o] * (S->u[i] - S->wR[o]);
+        }
+    }
+    for (int i = 0; i < N * S->ni; i++) SIGF(S->Ss[i], S->gs[i], S->vL[i], S->vU[i], S->s[i], S->clo[i], S->chi[i]);
+#undef SIGF
+    if (S->resto)
+        for (int r = 0; r < S->NR; r++) {
+            if (!row_el(S, r)) { S->Sp[r] = S->Sn[r] = INFINITY; S->gp[r] = S->gn[r] = S->rowr[r] = 0.0; continue; }
+            const double y = *row_y(S, r);
+            S->Sp[r] = S->zp[r] / S->pr[r];
+            S->Sn[r] = S->zn[r] / S->nr[r];
+            S->gp[r] = -mu / S->pr[r] + KAPPA_D * mu;
+            S->gn[r] = -mu / S->nr[r] + KAPPA_D * mu;
+            S->rowr[r] = (S->rho_r + S->gp[r] - y) / S->Sp[r] - (S->rho_r + S->gn[r] + y) / S->Sn[r];
+        }
+}
+
+/* IPOPT's inertia correction (IpPDPerturbationHandler.cpp get_deltas_for_wrong_inertia): delta_w = 0
+ * first; on wrong inertia 1e-4 if no earlier perturbation, else max(1e-20, last / 3); then x100 (no earlier
+ * one, or last far below) or x8 up to 1e40; a singular matrix first gets delta_c = 1e-8 mu^(1/4) */
+static int factor_f(ws_t *S, double mu, double *ic_last, int *n_ic, double *ts) {
+    double dw = 0.0, dc = (S->P->dc_always || S->O->dc_all) ? 1e-8 * pow(mu, 0.25) : 0.0;
+    const int ric = S->ric && !S->resto;
+    for (int tries = 0; tries < 200; tries++) {
+        const double t0 = wall_s();
+        const int fr = ric ? kkt_factor_ric(S, dw, dc, 0.0) : kkt_factor(S, dw, dc, 0.0);
+        ts[1] += wall_s() - t0;
+        if (fr == 0) {
+            if (dw > 0.0) *ic_last = dw;
+            return 1;
+        }
+        if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
+        (*n_ic)++;
+        if (dw == 0.0) dw = (*ic_last == 0.0) ? 1e-4 : fmax(1e-20, *ic_last / 3.0);
+        else dw *= (*ic_last == 0.0 || 1e5 * *ic_last < dw) ? 100.0 : 8.0;
+        if (dw > 1e40) return 0;
+    }
+    return 0;
+}
+
+static void direction_f(ws_t *S, double mu, const double *rdyn, const double *rin, const double *req) {
+    if (S->ric && !S->resto) kkt_direction_ric(S, mu, rdyn, rin, req);
+    else kkt_direction(S, mu, rdyn, rin, req);
+}
+
+/* primal step alpha, dual step az; bound multipliers kept within kappa_sigma = 1e10 of mu / slack */
+static void update_f(ws_t *S, double alpha, double az, double mu) {
+    const int N = S->N, nx = S->nx, nu = S->nu, ni = S->ni;
+    const size_t NX1 = (size_t)(N + 1) * nx, NU = (size_t)N * nu, NI = (size_t)N * ni, NE = (size_t)N * S->ne;
+    const double ks = 1e10;
+    for (size_t i = 0; i < NX1; i++) S->x[i] += alpha * S->dx[i];
+    for (size_t i = 0; i < NU; i++) S->u[i] += alpha * S->du[i];
+    for (size_t i = 0; i < NI; i++) { S->s[i] += alpha * S->ds[i]; S->yi[i] += alpha * S->dyi[i]; }
+    for (int i = 0; i < N * nx; i++) S->lam[i] += alpha * S->dlam[i];
+    for (size_t i = 0; i < NE; i++) S->ye[i] += alpha * S->dye[i];
+#define ZUPF(z, dz, slack)                                                                \
+    do {                                                                                  \
+        double zz = (z) + az * (dz), sl = (slack);                                        \
+        (z) = fmax(fmin(zz, ks * mu / sl), mu / (ks * sl));                               \
+    } while (0)
+    for (int k = 1; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            if (hasb(S->xlo[j])) ZUPF(S->zxL[i], S->dzxL[i], S->x[i] - S->xlo[j]);
+            if (hasb(S->xhi[j])) ZUPF(S->zxU[i], S->dzxU[i], S->xhi[j] - S->x[i]);
+        }
+    for (int i = 0; i < N * nu; i++) {
+        if (S->ufix[i]) continue;
+        if (hasb(S->ulo[i])) ZUPF(S->zuL[i], S->dzuL[i], S->u[i] - S->ulo[i]);
+        if (hasb(S->uhi[i])) ZUPF(S->zuU[i], S->dzuU[i], S->uhi[i] - S->u[i]);
+    }
+    for (int i = 0; i < N * ni; i++) {
+        if (hasb(S->clo[i])) ZUPF(S->vL[i], S->dvL[i], S->s[i] - S->clo[i]);
+        if (hasb(S->chi[i])) ZUPF(S->vU[i], S->dvU[i], S->chi[i] - S->s[i]);
+    }
+    if (S->resto)
+        for (int r = 0; r < S->NR; r++) {
+            if (!row_el(S, r)) continue;
+            S->pr[r] += alpha * S->dpr[r];
+            S->nr[r] += alpha * S->dnr[r];
+            ZUPF(S->zp[r], S->dzp[r], S->pr[r]);
+            ZUPF(S->zn[r], S->dzn[r], S->nr[r]);
+        }
+#undef ZUPF
+}
+
+static void eval_all(ws_t *S, double *ts) {
+    const double t0 = wall_s();
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int k = 0; k < S->N; k++) eval_derivs(S, k);
+    ts[0] += wall_s() - t0;
+    residuals_cached(S, S->rdyn, S->rin, S->req);
+}
+
+/* IPOPT's least-square constraint multipliers (DefaultIterateInitializer::least_square_mults, the
+ * restoration problem's start): min |grad f + J^T y - z|^2 through [[I, J^T], [J, 0]]; 0 if the system is
+ * singular or max |y| > constr_mult_init_max = 1000.  The derivatives of the current point must be
+ * evaluated; Sigma / gradients are overwritten (recomputed by barrier_f). */
+static void ls_mults(ws_t *S) {
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne;
+    const size_t NXN = (size_t)N * nx, NI = (size_t)N * ni, NE = (size_t)N * ne;
+    for (int k = 0; k < N; k++)
+        for (int a = 0; a < nv; a++)
+            for (int b = 0; b < nv; b++) S->W[(size_t)k * nv * nv + a * nv + b] = (a == b) ? 1.0 : 0.0;
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            S->Sx[i] = 0.0;
+            double g = -S->zxL[i] + S->zxU[i];
+            if (S->resto) g += S->zeta * S->dR[i] * (S->x[i] - S->wR[i]);
+            S->gx[i] = (k == 0) ? 0.0 : g;
+        }
+    if (N > 0) for (int j = 0; j < nx; j++) S->Sx[N * nx + j] = 1.0;  /* x_N's Hessian block is I too */
+    for (int i = 0; i < N * nu; i++) {
+        S->Su[i] = 0.0;
+        double g = -S->zuL[i] + S->zuU[i];
+        if (S->resto) g += S->zeta * S->dR[(N + 1) * nx + i] * (S->u[i] - S->wR[(N + 1) * nx + i]);
+        S->gu[i] = S->ufix[i] ? 0.0 : g;
+    }
+    for (size_t i = 0; i < NI; i++) { S->Ss[i] = 1.0; S->gs[i] = -S->vL[i] + S->vU[i]; }
+    if (S->resto)
+        for (int r = 0; r < S->NR; r++) {
+            const int el = row_el(S, r);
+            S->Sp[r] = S->Sn[r] = el ? 1.0 : INFINITY;
+            S->gp[r] = -S->zp[r]; S->gn[r] = -S->zn[r];
+            S->rowr[r] = el ? S->zn[r] - S->zp[r] : 0.0;  /* (rho - zp) - (rho - zn), y = 0 */
+        }
+    memset(S->lam, 0, NXN * sizeof(double));
+    memset(S->yi, 0, NI * sizeof(double));
+    memset(S->ye, 0, NE * sizeof(double));
+    double *z0 = dal(NXN + NI + NE);
+    int ok = (kkt_factor(S, 0.0, 0.0, 0.0) == 0);
+    if (ok) {
+        kkt_direction(S, 0.0, z0, z0 + NXN, z0 + NXN + NI);
+        double ym = 0;
+        for (size_t i = 0; i < NXN; i++) ym = fmax(ym, fabs(S->dlam[i]));
+        for (size_t i = 0; i < NI; i++) ym = fmax(ym, fabs(S->dyi[i]));
+        for (size_t i = 0; i < NE; i++) ym = fmax(ym, fabs(S->dye[i]));
+        if (ym <= 1e3) {
+            memcpy(S->lam, S->dlam, NXN * sizeof(double));
+            memcpy(S->yi, S->dyi, NI * sizeof(double));
+            memcpy(S->ye, S->dye, NE * sizeof(double));
+        }
+        if (S->O->verbose) fprintf(stderr, "   least-square multipliers: max |y| %.3e%s\n", ym, ym > 1e3 ? " -> 0" : "");
+    } else if (S->O->verbose) fprintf(stderr, "   least-square multipliers: singular system -> 0\n");
+    free(z0);
+}
+
+/* state of one IPOPT algorithm instance (the main problem, or the restoration problem) */
+typedef struct {
+    double mu, ic_last;
+    filt_t LS;
+    int in_wd, wd_short, wd_trial, n_wd;
+    double wd_ph, wd_th, wd_gd, wd_atest;
+    double *wd_it, *wd_dir;
+    int in_soft, soft_cnt, n_resto, n_soft;
+} fst_t;
+
+/* the restoration problem's link to the original one (RestoFilterConvergenceCheck) */
+typedef struct {
+    double mu_orig, th_R;
+    const filt_t *LSo;
+} resto_ctx;
+
+static int ls_orig_ok(const filt_t *L, double ph, double th) {
+    /* IsAcceptableToCurrentFilter && IsAcceptableToCurrentIterate(called_from_restoration = true) */
+    if (!isfinite(ph) || !isfinite(th)) return 0;
+    if (!(ls_le(th, (1.0 - 1e-5) * L->rth, L->rth) || ls_le(ph - L->rph, -1e-8 * L->rth, L->rph))) return 0;
+    for (int j = 0; j < L->nf; j++)
+        if (!(ph <= L->fph[j] || th <= L->fth[j])) return 0;
+    return 1;
+}
+
+static void fst_init(fst_t *F, double mu, size_t nit) {
+    memset(F, 0, sizeof *F);
+    F->mu = mu;
+    F->LS.theta_max = -1.0;
+    F->wd_it = dal(nit);
+    F->wd_dir = dal(nit);
+}
+static void fst_free(fst_t *F) { free(F->wd_it); free(F->wd_dir); free(F->LS.fph); free(F->LS.fth); }
+
+typedef struct {
+    int n_ls_fail, n_ic, n_soc;
+    double E0, cviol;
+    double ts[5];
+    size_t nit;
+} fcount_t;
+
+static int ipm_filter(ws_t *S, fst_t *F, int *it, fcount_t *C, const resto_ctx *R);
+
+/* TrySoftRestoStep: the full step min(alpha_primal, alpha_dual) for primal and dual variables, accepted if
+ * the original criteria accept it (then the soft phase ends) or it reduces the primal-dual system error by
+ * soft_resto_pderror_reduction_factor = 0.9999.  On success the iterate is updated in place. */
+static int soft_resto_step(ws_t *S, fst_t *F, double ap, double az, int *satisfies, fcount_t *C) {
+    const double a = fmin(ap, az), mu = F->mu;
+    double ph, th;
+    int ok;
+    *satisfies = 0;
+    trial_point(S, a);
+    merit_parts(S, S->tx, S->tu, S->ts, mu, &ph, &th, &ok, NULL, NULL, NULL);
+    if (ls_acceptable(&F->LS, 0.0, ph, th, ok)) {
+        *satisfies = 1;
+        update_f(S, a, a, mu);
+        return 1;
+    }
+    if (!ok) return 0;
+    errs_t E0;
+    opt_error_f(S, mu, &E0);
+    const double pd0 = E0.s1 / E0.n1;
+    double *buf = dal(C->nit);
+    copy_arrays(S, iter_arrays, buf, 1);
+    update_f(S, a, a, mu);
+    eval_all(S, C->ts);
+    errs_t E1;
+    opt_error_f(S, mu, &E1);
+    const double pd1 = E1.s1 / E1.n1;
+    if (S->O->verbose) fprintf(stderr, "   soft resto a %.3e pderr %.6e -> %.6e\n", a, pd0, pd1);
+    if (pd1 <= 0.9999 * pd0) { free(buf); return 1; }
+    copy_arrays(S, iter_arrays, buf, 0);
+    eval_all(S, C->ts);
+    free(buf);
+    return 0;
+}
+
+/* MinC_1NrmRestorationPhase::PerformRestoration: set up the restoration problem at the current point,
+ * solve it with the same algorithm until the original filter accepts its iterate with theta reduced to
+ * 0.9 theta_R, then return to the original problem with y = 0 (constr_mult_reset_threshold = 0) and the
+ * bound multipliers reset to 1 if any exceeds bound_mult_reset_threshold = 1000. */
+static int resto_phase(ws_t *S, fst_t *Fm, double thc, int *it, fcount_t *C) {
+    const int N = S->N, nx = S->nx, nu = S->nu, ni = S->ni, ne = S->ne;
+    const double rho = 1000.0;
+    const int ric_save = S->ric;
+    double cmax = 0;
+    for (int r = 0; r < S->NR; r++)
+        if (row_on(S, r)) {
+            const int nd = N * nx, nI = N * ni;
+            const double c = r < nd ? S->rdyn[r] : (r < nd + nI ? S->rin[r - nd] : S->req[r - nd - nI]);
+            cmax = fmax(cmax, fabs(c));
+        }
+    const double mu_r = fmax(Fm->mu, cmax);
+    for (int r = 0; r < S->NR; r++) {
+        if (!row_el(S, r)) { S->pr[r] = S->nr[r] = 1.0; S->zp[r] = S->zn[r] = 0.0; continue; }
+        const int nd = N * nx, nI = N * ni;
+        const double c = r < nd ? S->rdyn[r] : (r < nd + nI ? S->rin[r - nd] : S->req[r - nd - nI]);
+        const double a = (mu_r - rho * c) / (2.0 * rho);
+        S->nr[r] = a + sqrt(a * a + mu_r * c / (2.0 * rho));
+        S->pr[r] = c + S->nr[r];
+        S->zp[r] = mu_r / S->pr[r];
+        S->zn[r] = mu_r / S->nr[r];
+    }
+    for (int k = 0; k <= N; k++)
+        for (int j = 0; j < nx; j++) {
+            const int i = k * nx + j;
+            S->wR[i] = S->x[i];
+            S->dR[i] = 1.0 / fmax(1.0, S->x[i] * S->x[i]);
+        }
+    for (int i = 0; i < N * nu; i++) {
+        const int o = (N + 1) * nx + i;
+        S->wR[o] = S->u[i];
+        S->dR[o] = 1.0 / fmax(1.0, S->u[i] * S->u[i]);
+    }
+    /* bound multipliers of the original variables capped at rho */
+    double *zs[] = {S->zxL, S->zxU, S->zuL, S->zuU, S->vL, S->vU};
+    const size_t zl[] = {(size_t)(N + 1) * nx, (size_t)(N + 1) * nx, (size_t)N * nu, (size_t)N * nu, (size_t)N * ni,
+                         (size_t)N * ni};
+    for (int a = 0; a < 6; a++)
+        for (size_t i = 0; i < zl[a]; i++) zs[a][i] = fmin(zs[a][i], rho);
+    S->resto = 1; S->objw = 0.0; S->rho_r = rho; S->zeta = sqrt(mu_r); S->ric = 0;
+    eval_all(S, C->ts);
+    ls_mults(S);
+    fst_t Fr;
+    fst_init(&Fr, mu_r, C->nit);
+    resto_ctx R = {Fm->mu, thc, &Fm->LS};
+    if (S->O->verbose)
+        fprintf(stderr, "   ---- restoration phase: theta_R %.4e mu_R %.3e ----\n", thc, mu_r);
+    const int st = ipm_filter(S, &Fr, it, C, &R);
+    fst_free(&Fr);
+    S->resto = 0; S->objw = 1.0; S->ric = ric_save;
+    if (S->O->verbose) fprintf(stderr, "   ---- restoration phase end: status %d ----\n", st);
+    if (st != 0) return st;
+    memset(S->lam, 0, (size_t)N * nx * sizeof(double));
+    memset(S->yi, 0, (size_t)N * ni * sizeof(double));
+    memset(S->ye, 0, (size_t)N * ne * sizeof(double));
+    double zmax = 0;
+    for (int a = 0; a < 6; a++)
+        for (size_t i = 0; i < zl[a]; i++) zmax = fmax(zmax, zs[a][i]);
+    if (zmax > 1e3)
+        for (int a = 0; a < 6; a++)
+            for (size_t i = 0; i < zl[a]; i++)
+                if (zs[a][i] > 0.0) zs[a][i] = 1.0;
+    return 0;
+}
+
+/* IpoptAlgorithm::Optimize in filter mode: the main problem (R == NULL) or the restoration problem.
+ * Returns 0 converged (resto: the original filter accepted), 1 max_iter, 3 inertia / restoration failure,
+ * 4 restoration converged to a point of local infeasibility. */
+static int ipm_filter(ws_t *S, fst_t *F, int *it, fcount_t *C, const resto_ctx *R) {
+    const mfg_opts *O = S->O;
+    const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99;
+    const double mu_min = O->tol / (kappa_eps + 1.0);
+    for (; *it <= O->max_iter; (*it)++) {
+        eval_all(S, C->ts);
+        errs_t E;
+        opt_error_f(S, F->mu, &E);
+        const double E0 = fmax(fmax(E.dinf / E.sd, E.pinf), E.cinf0 / E.sc);
+        double Emu = fmax(fmax(E.dinf / E.sd, E.pinf), E.cinfm / E.sc);
+        if (O->verbose) {
+            double fo = 0;
+            for (int k = 0; k < S->N; k++) fo += S->l[k];
+            fprintf(stderr, "%sit %3d f %+.10e dinf %.2e pinf %.2e compl %.2e mu %.1e\n", R ? "r" : "", *it, fo,
+                    E.dinf, E.pinf, E.cinf0, F->mu);
+        }
+        if (!R) {
+            C->E0 = E0; C->cviol = E.pinf;
+            if (E0 <= O->tol && E.pinf <= O->constr_viol_tol) return 0;
+        } else {
+            double ph, th;
+            int ok;
+            merit_parts(S, S->x, S->u, S->s, R->mu_orig, &ph, &th, &ok, NULL, NULL, NULL);
+            if (O->verbose) fprintf(stderr, "   orig theta %.4e (resto start %.4e) phi %.8e\n", th, R->th_R, ph);
+            if (ok && th <= 0.9 * R->th_R && ls_orig_ok(R->LSo, ph, th)) return 0;
+            if (E0 <= O->tol) return 4;
+        }
+        if (*it == O->max_iter) return 1;
+        while (Emu <= kappa_eps * F->mu && F->mu > mu_min) {
+            const double mnew = fmax(mu_min, fmin(kappa_mu * F->mu, pow(F->mu, theta_mu)));
+            if (mnew >= F->mu) break;
+            F->mu = mnew;
+            F->LS.nf = 0;  /* MonotoneMuUpdate resets the line search's filter on every barrier update */
+            if (S->resto) S->zeta = sqrt(F->mu);
+            errs_t E2;
+            opt_error_f(S, F->mu, &E2);
+            Emu = fmax(fmax(E2.dinf / E2.sd, E2.pinf), E2.cinfm / E2.sc);
+        }
+        const double mu = F->mu, tau_fb = fmax(tau_min, 1.0 - mu);
+        barrier_f(S, mu);
+        if (!factor_f(S, mu, &F->ic_last, &C->n_ic, C->ts)) return 3;
+        double t_ph = wall_s();
+        direction_f(S, mu, S->rdyn, S->rin, S->req);
+        C->ts[2] += wall_s() - t_ph;
+        double ap, az;
+        ftb(S, tau_fb, &ap, &az);
+        /* ---- FindAcceptableTrialPoint ---- */
+        double phc, thc, gdc, pHp_unused;
+        int okc;
+        merit_parts_e(S, S->x, S->u, S->s, S->resto ? S->pr : NULL, S->resto ? S->nr : NULL, mu, &phc, &thc, &okc, NULL,
+                      NULL, NULL);
+        direction_model(S, &gdc, &pHp_unused);
+        if (F->LS.theta_max < 0.0) {
+            F->LS.theta_max = 1e4 * fmax(1.0, thc);
+            F->LS.theta_min = 1e-4 * fmax(1.0, thc);
+        }
+        double alpha = ap, atest = ap, pht = 0, tht = 0;
+        int accepted = 0, soc_used = 0, n_steps = 0, wd_step = 0, done = 0;
+        if (F->in_soft) {  /* soft restoration phase: at most max_soft_resto_iters = 10 iterations */
+            F->LS.rph = phc; F->LS.rth = thc; F->LS.rgd = gdc;
+            int sat = 0;
+            if (++F->soft_cnt <= 10 && soft_resto_step(S, F, ap, az, &sat, C)) {
+                if (sat) { F->in_soft = 0; F->soft_cnt = 0; }
+                F->n_soft++;
+                if (O->verbose) fprintf(stderr, "   soft resto step (%s)\n", sat ? "S" : "s");
+                continue;
+            }
+            F->in_soft = 0;
+            if (R) return 3;
+            F->n_resto++;
+            const int st = resto_phase(S, F, thc, it, C);
+            if (st) return st;
+            F->in_wd = 0; F->wd_short = 0;
+            continue;
+        }
+        if (!F->in_wd && F->wd_short >= 10) {  /* StartWatchDog */
+            F->in_wd = 1; F->wd_trial = 0; F->n_wd++;
+            F->wd_ph = phc; F->wd_th = thc; F->wd_gd = gdc; F->wd_atest = ap;
+            copy_arrays(S, iter_arrays, F->wd_it, 1);
+            copy_arrays(S, dir_arrays, F->wd_dir, 1);
+        }
+        F->LS.rph = F->in_wd ? F->wd_ph : phc;
+        F->LS.rth = F->in_wd ? F->wd_th : thc;
+        F->LS.rgd = F->in_wd ? F->wd_gd : gdc;
+        accepted = filter_backtrack(S, &F->LS, mu, tau_fb, ap, thc, 0, F->in_wd, F->wd_atest, &alpha, &az, &atest,
+                                    &n_steps, &soc_used, &pht, &tht, C->ts);
+        if (F->in_wd) {
+            if (accepted) F->in_wd = 0;
+            else if (++F->wd_trial > 3) {  /* StopWatchDog: back to the stored point, backtrack from alpha_max/2 */
+                F->in_wd = 0; F->wd_short = 0;
+                copy_arrays(S, iter_arrays, F->wd_it, 0);
+                copy_arrays(S, dir_arrays, F->wd_dir, 0);
+                eval_all(S, C->ts);  /* value caches of the stored point */
+                ftb(S, tau_fb, &ap, &az);
+                F->LS.rph = F->wd_ph; F->LS.rth = F->wd_th; F->LS.rgd = F->wd_gd;
+                merit_parts_e(S, S->x, S->u, S->s, S->resto ? S->pr : NULL, S->resto ? S->nr : NULL, mu, &phc, &thc,
+                              &okc, NULL, NULL, NULL);
+                accepted = filter_backtrack(S, &F->LS, mu, tau_fb, ap, thc, 1, 0, 0.0, &alpha, &az, &atest, &n_steps,
+                                            &soc_used, &pht, &tht, C->ts);
+            } else {  /* the watchdog's full trial step, no filter update */
+                accepted = 1; wd_step = 1; alpha = ap; n_steps = 0;
+            }
+        }
+        if (accepted && !wd_step && (!ls_ftype(&F->LS, atest) || !ls_armijo(&F->LS, atest, pht))) ls_augment(&F->LS);
+        if (O->verbose)
+            fprintf(stderr, "   ap %.3e az %.3e alpha %.3e acc %d soc %d steps %d wd %d/%d filt %d th %.3e ph %.10e\n",
+                    ap, az, alpha, accepted, soc_used, n_steps, F->in_wd, F->wd_trial, F->LS.nf, thc, phc);
+        if (!accepted) {
+            C->n_ls_fail++;
+            if (R) return 3;  /* no restoration inside the restoration phase */
+            /* PrepareRestoPhaseStart augments the filter with the current point; then the soft restoration
+             * phase is tried, and the restoration phase if its step fails */
+            F->LS.rph = phc; F->LS.rth = thc; F->LS.rgd = gdc;
+            ls_augment(&F->LS);
+            ftb(S, tau_fb, &ap, &az);
+            int sat = 0;
+            if (soft_resto_step(S, F, ap, az, &sat, C)) {
+                F->in_soft = !sat; F->soft_cnt = 0; F->n_soft++;
+                if (O->verbose) fprintf(stderr, "   soft resto start (%s)\n", sat ? "S" : "s");
+                continue;
+            }
+            F->n_resto++;
+            const int st = resto_phase(S, F, thc, it, C);
+            if (st) return st;
+            F->in_wd = 0; F->wd_short = 0;
+            continue;
+        }
+        (void)done;
+        C->n_soc += soc_used;
+        if (!F->in_wd) F->wd_short = (n_steps == 0) ? 0 : F->wd_short + 1;
+        update_f(S, alpha, az, mu);
+    }
+    return 1;
 }
 
 int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const mfg_opts *O, double *w_out,
@@ -1159,6 +1985,17 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     }
     S->perm = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
     S->piv = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
+    S->objw = 1.0;
+    S->NR = (int)((size_t)N * nx + NI + NE);
+    const size_t NIT4 = 3 * NX1 + 3 * NU + 4 * NI + (size_t)N * nx + NE + 4 * (size_t)S->NR;
+    if (O->filter) {  /* restoration-phase arrays; direction / iterate copies with the elastic variables */
+        double **ra[] = {&S->pr, &S->nr, &S->zp, &S->zn, &S->dpr, &S->dnr, &S->dzp, &S->dzn, &S->tpr, &S->tnr,
+                         &S->Sp, &S->Sn, &S->gp, &S->gn, &S->rowr};
+        for (size_t i = 0; i < sizeof ra / sizeof ra[0]; i++) *ra[i] = dal(S->NR);
+        S->wR = dal(NX1 + NU); S->dR = dal(NX1 + NU);
+        free(S->bk);
+        S->bk = dal(NIT4);
+    }
 
     /* ---- initial point (IPOPT: x0 = 0 or the held state, bound_push / bound_frac = 1e-2) ---- */
     for (int k = 0; k <= N; k++)
@@ -1227,6 +2064,21 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     const int has_tier1 = P->tier1_to > P->tier1_from;
 
     double ts[5] = {0, 0, 0, 0, 0}, t_solve0 = wall_s(), t_ph;
+    if (O->filter) {  /* IPOPT's globalisation (mfg_opts.filter) */
+        fcount_t C;
+        memset(&C, 0, sizeof C);
+        C.nit = NIT4; C.E0 = INFINITY; C.cviol = INFINITY;
+        fst_t F;
+        fst_init(&F, O->mu_init, C.nit);
+        it = 0;
+        status = ipm_filter(S, &F, &it, &C, NULL);
+        mu = F.mu; E0 = C.E0; cviol = C.cviol; n_ls_fail = C.n_ls_fail; n_ic = C.n_ic; n_soc = C.n_soc;
+        for (int i = 0; i < 4; i++) ts[i] += C.ts[i];
+        if (O->verbose)
+            fprintf(stderr, "filter: watchdogs %d soft-restoration steps %d restoration phases %d\n", F.n_wd, F.n_soft,
+                    F.n_resto);
+        fst_free(&F);
+    } else
     for (it = 0; it <= O->max_iter; it++) {
         /* ---- node derivatives ---- */
         t_ph = wall_s();
@@ -1537,6 +2389,11 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     for (size_t i = 0; i < sizeof pp / sizeof pp[0]; i++) free(*pp[i]);
     free(S->ufix); free(S->perm); free(S->piv);
     if (S->ric) { free(S->Pg); free(S->Kst); free(S->Fg); free(S->pvg); free(S->kvg); free(S->Kpp); }
+    if (O->filter) {
+        double **ra[] = {&S->pr, &S->nr, &S->zp, &S->zn, &S->dpr, &S->dnr, &S->dzp, &S->dzn, &S->tpr, &S->tnr,
+                         &S->Sp, &S->Sn, &S->gp, &S->gn, &S->rowr, &S->wR, &S->dR};
+        for (size_t i = 0; i < sizeof ra / sizeof ra[0]; i++) free(*ra[i]);
+    }
     return 0;
 }
 

@@ -24,7 +24,7 @@ static void run(const DevModel *M, const DevFrame *F, const GParams &P, const do
     for (int i = 0; i < D::NE; i++) yev[i] = ye[i];
     for (int i = 0; i < D::NM; i++) yev[D::NEA + i] = ye[D::NE + i];
     for (int t = 0; t < FAM::PRE; t++) FAM::prepass(M, F, P, x, u, t, S);
-    FAM::seeds(P, u, yi, yev, lam, true, S);
+    FAM::seeds(P, u, yi, yev, lam, true, 1.0, S);
     for (int t = 0; t < FAM::LANES; t++) FAM::lane(M, F, x, u, yi, t, S);
     for (int e = 0; e < D::REC; e++) rec[e] = FAM::rec(P, x, u, yi, yev, lam, true, S, e, lref);
 }

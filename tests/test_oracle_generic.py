@@ -6,6 +6,8 @@
   reference's committed IPOPT solutions plotter/solution.csv (G1, N=50) and plotter/Result_2 (G2,
   N=80) to 1e-6 rad (measured 1e-8), and Result_1 (G4, both arms +-500).  The decision-vector layout
   [x_0 | (u_k, x_{k+1})] is the reference's CSV layout, so the CSVs compare entry by entry.
+* IPOPT mode (mfg_opts.filter): solved as the reference solves it -- x0 = 0, no homotopy -- the oracle reproduces
+  G1 and G4 (and G2, tools/ipopt_mode_probe.py) to 1e-6 rad; G3 lands in a neighbouring minimum (lower objective).
 * Result_4 (G3, both arms phase-limited) is a KKT point of the build's transcription: started there with
   IPOPT's warm_start_init_point constants (bound push 1e-3, bound multipliers 1e-3) and mu_0 = 1e-3 the
   oracle converges back to it within 1e-6 rad with the same objective.  Its torque rows sit outside the
@@ -103,6 +105,35 @@ def test_box_resolve_matches_reference_trajectory(golden, name, kw):
     assert dq < 1e-6, dq
     # the whole vector satisfies the reference problem at the IPOPT tolerance
     assert res[-1].cviol < 1e-8
+
+
+IPOPT_MODE = dict(init_zero=True, bound_relax=1e-8, max_iter=1500, max_soc=4, filter=True, resto_hard_dyn=True)
+
+
+@pytest.mark.parametrize("name,kw", [("G1_box_N50", dict(N=50)), ("G4_box_N80", dict(N=80, right_const=False))])
+def test_box_ipopt_mode_cold_solve_matches_reference(golden, name, kw):
+    """Box_Pilz_6DOF.py solved as L455-456 do -- IPOPT from x0 = 0, no homotopy -- with IPOPT's globalisation in
+    the oracle (mfg_opts.filter: filter line search, watchdog, soft restoration, restoration phase; bound_relax_factor
+    1e-8): the joint trajectory equals the reference's (G1 plotter/solution.csv, G4 Result_1) to 1e-6 rad (measured
+    5e-9 / 1.5e-9).  G2 is the same at 1e-11 (tools/ipopt_mode_probe.py; left out here for the suite's time)."""
+    g, N = golden[name]
+    w, r = G.solve(PR.box_dual(q0=g[:12], **kw), **IPOPT_MODE)
+    assert r.status == 0, (r.status, r.iter)
+    assert np.abs(q_traj(w, N) - q_traj(g, N)).max() < 1e-6
+    assert r.n_ls_fail > 0  # the path goes through IPOPT's restoration phase (x0 = 0 is far from feasible)
+
+
+def test_box_g3_ipopt_mode_cold_solve(golden):
+    """G3 (Result_4, LeftConst) from x0 = 0 in IPOPT mode converges to a neighbouring local minimum: objective
+    1505.984 against G3's 1506.778 (lower), at most 0.03 rad away, every constraint satisfied.  The problem has
+    several KKT points within 0.03 rad and 0.1 % of the objective; which one IPOPT's own path reached
+    depends on details of its MUMPS factorisation this restatement cannot reproduce."""
+    g, N = golden["G3_box_N80"]
+    w, r = G.solve(PR.box_dual(q0=g[:12], N=N, left_const=True), **IPOPT_MODE)
+    assert r.status == 0 and r.cviol < 1e-8
+    f_g3 = _g3_objective(g, N)
+    assert r.obj < f_g3 and abs(r.obj - f_g3) < 1e-3 * f_g3
+    assert np.abs(q_traj(w, N) - q_traj(g, N)).max() < 0.05
 
 
 def _g3_objective(g, N):
