@@ -256,6 +256,11 @@ int mf_gnode_record(mf_gproblem *p, const double *xu, const double *yi, const do
 /* Diagnostics: dual state of problem b after the last solve, [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU |
  * mu] (per-node blocks as the solver stores them).  Returns the number of doubles written. */
 int mf_gdebug_duals(mf_gproblem *p, int b, double *out);
+/* Diagnostics: IPOPT-mode trace of horizon 0 of the last solve made with opts.verbose >= 2, 2 x 4096 rows of 16
+ * doubles (rows of the phase-0 kernel, then of the line-search kernel, indexed by iteration); returns 4096.
+ * _reset zeroes it. */
+int mf_gdebug_trace(double *out);
+int mf_gdebug_trace_reset(void);
 
 const char *mf_last_error(void);
 

@@ -61,7 +61,7 @@ struct GParams {
     int target_decimals;                   // CentauroFam: round the relative-pose targets (-1: exact)
     int dc_always;                         // delta_c from the first factorisation (rank-deficient rows)
     int filter;                            // IPOPT's globalisation (filter, watchdog, restoration; gipm.hip)
-    int pad_f;
+    int dbg;                               // trace horizon 0 (diagnostics, gipm.hip mf_gdebug_trace)
 };
 
 template <int NX_, int NU_, int NI_, int NE_, int NM_ = 0> struct GDims {

@@ -56,6 +56,10 @@ enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INER
 //                  the next iteration re-evaluates (and then sets up the restoration)
 enum { GP_NONE = 0, GP_SOFT = 1, GP_RESTO = 2, GP_LSM = 3, GP_IDLE = 4, GP_IDLE_RESTO = 5 };
 constexpr int GFCAP = 512;  // filter entries per filter (dominated entries are dropped as IPOPT does)
+// diagnostic trace of horizon 0 in IPOPT mode (mf_gopts.verbose >= 2; mf_gdebug_trace): per iteration one row
+// from k_gpre (E_0 pieces, the restoration exit test) and one from k_gls (line search)
+constexpr int GDBG_ROWS = 4096, GDBG_W = 16;
+__device__ double mf_gdbg_pre[GDBG_ROWS * GDBG_W], mf_gdbg_ls[GDBG_ROWS * GDBG_W];
 
 struct GArrays {
     double *x, *u, *s, *lam, *ye, *yi, *zxL, *zxU, *zuL, *zuU, *vL, *vU;
@@ -843,7 +847,16 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             }
             return;
         }
+        if (P.dbg && b == 0 && lane == 0 && st.iter < GDBG_ROWS) {
+            double *t = mf_gdbg_pre + st.iter * GDBG_W;
+            t[8] = tho; t[9] = pho; t[10] = oko; t[11] = st.rs_th; t[12] = st.rs_ph; t[13] = cur_ok;
+        }
         if (E0 <= P.tol) { finish(GS_LOCINF); return; }
+    }
+    if (P.dbg && b == 0 && lane == 0 && st.iter < GDBG_ROWS) {
+        double *t = mf_gdbg_pre + st.iter * GDBG_W;
+        t[0] = st.iter; t[1] = st.mode; t[2] = mu; t[3] = E0; t[4] = pinf; t[5] = dinf; t[6] = Eq.cinf0; t[7] = st.nf[0];
+        t[14] = st.nf[1]; t[15] = st.n_resto;
     }
     if (st.iter >= P.max_iter) { finish(GS_MAXITER); return; }
     const double mu_min = flt ? P.tol / (kappa_eps + 1.0) : P.tol / 10.0;
@@ -1804,6 +1817,10 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         }
     }
     if (want_soft) {
+        // the point a restoration would start from (MinC_1NrmRestorationPhase's reference): this iteration's, also
+        // when k_gpre undoes the pending step
+        st.rs_ph = phc;
+        st.rs_th = thc;
         double a = 0.0;
         const int r = soft_step(a);
         if (r == 0) {
@@ -1827,6 +1844,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         st.in_soft = 0;
         st.soft_cnt = 0;
         st.pend = GP_RESTO;
+    }
+    if (P.dbg && b == 0 && lane == 0 && st.iter < GDBG_ROWS) {
+        double *t = mf_gdbg_ls + st.iter * GDBG_W;
+        t[0] = st.iter; t[1] = m; t[2] = thc; t[3] = phc; t[4] = gdc; t[5] = ap; t[6] = az; t[7] = step_a;
+        t[8] = do_step; t[9] = want_soft; t[10] = go_resto; t[11] = st.nf[0]; t[12] = st.nf[1]; t[13] = st.in_wd;
+        t[14] = st.pend; t[15] = st.in_soft;
     }
     if (do_step) apply_step(step_a, step_az);
     store();
@@ -2136,6 +2159,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     P.max_soc = o ? o->max_soc : 4;
     P.warm_start = (o && d_w0) ? o->warm_start : 0;
     P.filter = o ? o->filter : 0;
+    P.dbg = (o && o->verbose >= 2) ? 1 : 0;
     p->last_batch = batch;
     // IPOPT bound_relax_factor: every finite bound of a non-fixed variable or row moves out by
     // br max(1, |b|) (oracle/mf_ocp.c, same rule); fixed controls (lo == hi) stay parameters
@@ -2464,6 +2488,21 @@ extern "C" int mf_debug_gstamps_reset(void) {
     return hipMemcpyToSymbol(HIP_SYMBOL(mf::mf_gstamp_buf), z, sizeof z) == hipSuccess ? 0 : -1;
 }
 #endif
+
+// diagnostics: the IPOPT-mode trace of horizon 0 of the last solve with verbose >= 2 (rows of GDBG_W doubles:
+// rows [0, GDBG_ROWS) from k_gpre, then [GDBG_ROWS, 2 GDBG_ROWS) from k_gls, indexed by the iteration)
+extern "C" int mf_gdebug_trace(double *out) {
+    if (!out) return capi_fail(MF_ERR_ARG, "null argument");
+    GHIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(mf_gdbg_pre), sizeof(double) * GDBG_ROWS * GDBG_W));
+    GHIPCHK(hipMemcpyFromSymbol(out + GDBG_ROWS * GDBG_W, HIP_SYMBOL(mf_gdbg_ls), sizeof(double) * GDBG_ROWS * GDBG_W));
+    return GDBG_ROWS;
+}
+extern "C" int mf_gdebug_trace_reset(void) {
+    static std::vector<double> z((size_t)GDBG_ROWS * GDBG_W, 0.0);
+    GHIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(mf_gdbg_pre), z.data(), sizeof(double) * z.size()));
+    GHIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(mf_gdbg_ls), z.data(), sizeof(double) * z.size()));
+    return MF_OK;
+}
 
 extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {
     if (!p || !out) return capi_fail(MF_ERR_ARG, "null argument");

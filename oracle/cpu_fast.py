@@ -39,7 +39,8 @@ class GParams(C.Structure):
                 ("tol", C.c_double), ("constr_viol_tol", C.c_double), ("mu_init", C.c_double), ("F_init", C.c_double),
                 ("max_iter", C.c_int), ("max_soc", C.c_int), ("init_zero", C.c_int), ("has_u_init", C.c_int),
                 ("warm_start", C.c_int), ("pad_ws", C.c_int), ("u_init", C.c_double * GX), ("force_from", C.c_int), ("tier1_from", C.c_int),
-                ("tier1_to", C.c_int), ("target_decimals", C.c_int), ("dc_always", C.c_int)]
+                ("tier1_to", C.c_int), ("target_decimals", C.c_int), ("dc_always", C.c_int),
+                ("filter", C.c_int), ("dbg", C.c_int)]
 
 
 def gparams(spec: dict) -> GParams:

@@ -47,3 +47,23 @@ def test_no_device_function_calls(tmp_path):
         assert "s_endpgm" in asm
         calls += asm.count("s_swappc_b64")
     assert calls == 0, f"{calls} device function calls (s_swappc_b64) in the gfx950 code objects"
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump missing")
+def test_no_dynamic_stack(tmp_path):
+    """No kernel may need a dynamic stack (a call the compiler cannot bound, or recursion): its private segment
+    would be sized at run time.  Round 3's aperture-violation kernel had a real call."""
+    readelf = os.path.join(os.path.dirname(OBJDUMP), "llvm-readelf")
+    checked = 0
+    for i, o in enumerate(_gfx950_objects(LIB)):
+        f = tmp_path / f"co{i}.o"
+        f.write_bytes(o)
+        notes = subprocess.run([readelf, "--notes", str(f)], capture_output=True, text=True, check=True).stdout
+        kernels = notes.split(".agpr_count:")[1:]
+        for k in kernels:
+            m = re.search(r"\.name:\s+(\S+)", k)
+            if not m:
+                continue
+            checked += 1
+            assert not re.search(r"\.uses_dynamic_stack:\s+true", k), m.group(1)
+    assert checked > 0

@@ -4,10 +4,14 @@ perturbed initial states (bench.py imports generic_extra for its `generic` keys;
     python tools/generic_bench.py [--batch 1024] [--sample 2]
 
 C3-shared: problems.box_shared_fatigue(N=100) from the reference's IK start q0 (tests/golden G1) with
-  q0_i = q0 + U(-0.01, 0.01) per joint; the equilibrium-tolerance homotopy (pos_toll 1 -> 1e-2 -> 1e-4,
-  each stage warm-started from the previous one), i.e. what GOCP.solve_box does, timed end to end.
+  q0_i = q0 + U(-0.01, 0.01) per joint.
 C4: problems.centauro(N=50, T=2) (the committed Centauro fixture's horizon, Centauro_dynamics.py:90-91)
-  from the IK start with q0_i = q0 + U(-0.02, 0.02), one solve from the reference's sol0 controls.
+  from the IK start with q0_i = q0 + U(-0.02, 0.02).
+mode "ipopt" (default): one solve per horizon as the reference makes it -- IPOPT from x0 = 0 (Box_Pilz_6DOF.py:
+  455-456 and the first solve of RepeatedMPCwithThermal.py:464-466 pass no x0), with IPOPT's globalisation
+  (mf_gopts.filter: filter line search, watchdog, soft restoration, restoration phase) and bound_relax_factor 1e-8.
+mode "merit": round 3's figure -- the l1-merit search, C3 through the pos_toll homotopy 1 -> 1e-2 -> 1e-4 from
+  F = (0, 0, m g / 2), C4 from the reference's sol0 controls.
 A horizon counts when its last stage converged (E_0 <= 1e-8).  GPU-vs-CPU: the first `sample` horizons
 solved by the host IPM (oracle/libmfcpu.so, the same algorithm) and compared on the state trajectories.
 """
@@ -42,9 +46,12 @@ def _x_traj(w, nx, nu, N):
     return np.concatenate([w[:, None, :nx], w[:, nx:].reshape(w.shape[0], N, nu + nx)[:, :, nu:]], axis=1)
 
 
+IPOPT_KW = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=1500, max_soc=4)
+
+
 def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0, cases=("c3", "c4"),
-                  stage_caps=None, batch_c4: int | None = None) -> dict:
-    """stage_caps: iteration caps of the C3 homotopy stages (default: 1000 each, GOCP.solve_box's)."""
+                  stage_caps=None, batch_c4: int | None = None, mode: str = "ipopt") -> dict:
+    """stage_caps: iteration caps of the C3 homotopy stages (merit mode; default: 1000 each, GOCP.solve_box's)."""
     import torch
 
     from mpc_fatigue_amd import problems as PR
@@ -59,13 +66,19 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
     q0b = _golden_q0()
     sp3 = PR.box_shared_fatigue(N=100, q0=q0b)
     X3 = np.hstack([q0b[None] + rng.uniform(-0.01, 0.01, (batch, 12)), np.tile(sp3["T0"], (batch, 1))])
-    cases.append(("c3_shared_budget_n100", sp3, X3, [dict(sp3, pos_toll=t) for t in PR.box_homotopy_tolerances()],
-                  dict(u_init=PR.box_u_init(sp3), max_iter=1000, max_soc=4)))
+    if mode == "ipopt":
+        cases.append(("c3_shared_budget_n100", sp3, X3, [sp3], dict(IPOPT_KW)))
+    else:
+        cases.append(("c3_shared_budget_n100", sp3, X3, [dict(sp3, pos_toll=t) for t in PR.box_homotopy_tolerances()],
+                      dict(u_init=PR.box_u_init(sp3), max_iter=1000, max_soc=4)))
     sp4 = PR.centauro(N=50, T=2.0)
     q0c = np.asarray(sp4["q0"])
     b4 = batch_c4 or batch
     X4 = np.hstack([q0c[None] + rng.uniform(-0.02, 0.02, (b4, 14)), np.tile(sp4["T0"], (b4, 1))])
-    cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(u_init=PR.centauro_u_init(sp4), max_iter=500, max_soc=4)))
+    if mode == "ipopt":
+        cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(IPOPT_KW)))
+    else:
+        cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(u_init=PR.centauro_u_init(sp4), max_iter=500, max_soc=4)))
     cases = [c for c in cases if c[0][:2] in todo]
     for name, spec, X, stages, kw in cases:
         batch = X.shape[0]
@@ -99,7 +112,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
         st = bufs[-1]["status"].cpu().numpy()
         its = [int(b["iters"].sum().item()) for b in bufs]
         conv = int((st == 0).sum())
-        rec = {"value": conv / dt, "unit": "horizons/s", "batch": batch, "converged": conv,
+        rec = {"mode": mode, "value": conv / dt, "unit": "horizons/s", "batch": batch, "converged": conv,
                "converged_frac": conv / batch, "seconds": dt, "stages": len(stages),
                "mean_iters_per_stage": [i / batch for i in its], "stage_max_iter": caps,
                "N": N, "nx": nx, "nu": nu, "ni": gs[0].ni}
@@ -115,6 +128,8 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
                 specs = [dict(st_spec, q0=list(X[i, :len(spec["q0"])]), T0=list(X[i, len(spec["q0"]):]))
                          for i in range(sample)]
                 kwc = dict(kw, max_iter=cap, riccati=True, **fk.opts_kw())
+                if kw.get("filter"):
+                    kwc["resto_hard_dyn"] = True  # the device's restoration problem (exact dynamics rows)
                 res = [G.solve_batch([sp_], nthreads=1, L=CF.lib(), w0=(None if w is None else w[i]), **kwc)
                        for i, sp_ in enumerate(specs)]
                 w = np.vstack([r[0] for r in res])
@@ -139,8 +154,9 @@ if __name__ == "__main__":
     ap.add_argument("--cases", default="c3,c4", help="comma list of c3 (shared budget N=100) and c4 (Centauro N=50)")
     ap.add_argument("--sample", type=int, default=2)
     ap.add_argument("--caps", default="", help="comma list of C3 homotopy stage iteration caps (default 1000 each)")
+    ap.add_argument("--mode", default="ipopt", choices=["ipopt", "merit"])
     a = ap.parse_args()
     import torch
     torch.cuda.init()
     caps = [int(c) for c in a.caps.split(",")] if a.caps else None
-    print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")), stage_caps=caps)))
+    print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")), stage_caps=caps, mode=a.mode)))

@@ -30,3 +30,18 @@ for c in (sys.argv[1:] or list(CASES)):
     out[c] = r.w[0]
 os.makedirs(os.path.join(HERE, "gpurun_out"), exist_ok=True)
 np.savez(os.path.join(HERE, "gpurun_out", "ipopt_mode_probe.npz"), **out)
+
+if os.environ.get("MF_TRACE_CASE"):  # per-iteration device trace of one case (verbose >= 2)
+    import ctypes as C
+    from mpc_fatigue_amd import _lib
+    c = os.environ["MF_TRACE_CASE"]
+    name, kw = CASES[c]
+    g = read_solution_csv(os.path.join(HERE, "tests", "golden", name + "_solution.csv"))
+    ocp = GOCP(PR.box_dual(q0=g[:12], **kw))
+    _lib.lib().mf_gdebug_trace_reset()
+    r = ocp.solve(init_zero=True, bound_relax=1e-8, filter=True, max_iter=int(os.environ.get("MF_TRACE_ITERS", "1500")),
+                  max_soc=4, verbose=2)
+    buf = np.zeros(2 * 4096 * 16)
+    _lib.lib().mf_gdebug_trace(buf.ctypes.data_as(C.POINTER(C.c_double)))
+    np.save(os.path.join(HERE, "gpurun_out", f"trace_{c}.npy"), buf.reshape(2, 4096, 16))
+    print("trace", c, int(r.status[0]), int(r.iters[0]))
