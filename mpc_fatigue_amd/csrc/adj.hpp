@@ -101,7 +101,7 @@ MF_HD void fwd_range(const DevModel &M, int i0, int i1, const In &in, const doub
     TV(&w)[3] = S.w; TV(&dw)[3] = S.dw; TV(&a)[3] = S.a;
 #pragma unroll 1
     for (int i = i0; i < i1; i++) {
-        const DevJoint &J = M.j[i];
+        const DevJoint &J = joint_at(M, i);
         TP A[9], on[3], z[3];
         if (i == 0) {
 #pragma unroll
@@ -154,7 +154,7 @@ MF_HD void rev_range(const DevModel &M, const DevFrame &F, int fp, int i_hi, int
     TV(&G)[3] = S.G; TV(&Ob)[3] = S.Ob;
 #pragma unroll 1
     for (int i = i_hi; i >= i_lo; i--) {
-        const DevJoint &J = M.j[i];
+        const DevJoint &J = joint_at(M, i);
         const double m = J.m;
         const TV qdi = as_tv<TV>(in.qd(i));
         TP z[3];

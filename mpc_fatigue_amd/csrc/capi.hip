@@ -385,10 +385,13 @@ static int dalloc(DBuf &b, size_t n) {
     HIPCHK(hipMalloc(&b.p, (n ? n : 1) * sizeof(double)));
     return MF_OK;
 }
-static int h2d(DBuf &b, const double *h, size_t n) {
+// upload: on `s` when given (ordered before the launches on that stream by the stream itself), else the
+// blocking copy the single-stream bridge functions use
+static int h2d(DBuf &b, const double *h, size_t n, hipStream_t s = nullptr) {
     int e = dalloc(b, n);
     if (e) return e;
-    if (n) HIPCHK(hipMemcpy(b.p, h, n * sizeof(double), hipMemcpyHostToDevice));
+    if (n && s) HIPCHK(hipMemcpyAsync(b.p, h, n * sizeof(double), hipMemcpyHostToDevice, s));
+    else if (n) HIPCHK(hipMemcpy(b.p, h, n * sizeof(double), hipMemcpyHostToDevice));
     return MF_OK;
 }
 
@@ -688,17 +691,17 @@ static int solve_host(mf_problem *p, int batch, const double *q0, const double *
     const int n = p->C.n, ws = mf_problem_wsize(p);
     DBuf dq0, dqd0, dw0, dl, dw, dk, dob;
     IBuf dst, dit;
-    if ((e = h2d(dq0, q0, (size_t)n * batch))) return e;
-    if (qd0 && (e = h2d(dqd0, qd0, (size_t)n * batch))) return e;
-    if (w0 && (e = h2d(dw0, w0, (size_t)ws * batch))) return e;
-    if (line_ref && (e = h2d(dl, line_ref, 2 * (size_t)batch))) return e;
+    // a stream of this call's own: uploads, solve and copies back are ordered on it and synchronise with
+    // it alone, so host calls on other handles / streams of the device keep running (reentrant)
+    OwnStream os;
+    HIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
+    if ((e = h2d(dq0, q0, (size_t)n * batch, os.s))) return e;
+    if (qd0 && (e = h2d(dqd0, qd0, (size_t)n * batch, os.s))) return e;
+    if (w0 && (e = h2d(dw0, w0, (size_t)ws * batch, os.s))) return e;
+    if (line_ref && (e = h2d(dl, line_ref, 2 * (size_t)batch, os.s))) return e;
     if ((e = dalloc(dw, (size_t)ws * batch)) || (e = dalloc(dk, batch)) || (e = dalloc(dob, batch))) return e;
     HIPCHK(hipMalloc(&dst.p, sizeof(int) * batch));
     HIPCHK(hipMalloc(&dit.p, sizeof(int) * batch));
-    // a stream of this call's own: the solve and the copies back synchronise with it alone, so host
-    // calls on other handles / streams of the device keep running (one handle per stream, reentrant)
-    OwnStream os;
-    HIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
     e = solve_core(p, batch, dq0.p, dqd0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst.p, dit.p, dk.p, dob.p,
                    os.s);
     if (e) return e;

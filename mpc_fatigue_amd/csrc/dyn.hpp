@@ -28,6 +28,23 @@
 
 #define MF_HD __host__ __device__ __forceinline__
 
+// Joint i of a model as a pointer of its own.  A descending joint loop otherwise lets the compiler strength-
+// reduce &M.j[i] to a base of &M.j[NJ-1] - 400 (NJ-1-i) bytes and fold the constant into the instruction's
+// offset.  For a model image in LDS read through a generic pointer (the phase kernels' images, gipm.hip), that
+// base register then lies below the start of the LDS aperture whenever the image sits within a few joint
+// records of LDS offset 0, and the flat load raises MEMORY_APERTURE_VIOLATION: the aperture of a flat access
+// is decided on its base register, not on base + offset (tools/gchk_run.py).
+// Only a translation unit whose kernels read model images through generic pointers (gipm.hip: the images are
+// selected per arm, MArr) defines MF_GENERIC_MODEL_PTR; elsewhere the images are plain __shared__ objects, the
+// loads are LDS instructions, and the pointer stays transparent.
+template <class M_> MF_HD const auto &joint_at(const M_ &M, int i) {
+    const auto *p = &M.j[i];
+#if defined(__HIP_DEVICE_COMPILE__) && defined(MF_GENERIC_MODEL_PTR)
+    __asm__ volatile("" : "+v"(p));
+#endif
+    return *p;
+}
+
 namespace mf {
 
 // ---------------------------------------------------------------- scalars
@@ -165,7 +182,7 @@ MF_HD void ne_pass(const DevModel &M, int n, const T *q, const T *qd, const T *q
     for (int k = 0; k < 9; k++) R[k] = T((k % 4) == 0 ? 1.0 : 0.0);
 #pragma unroll
     for (int i = 0; i < n; i++) {
-        const DevJoint &J = M.j[i];
+        const DevJoint &J = joint_at(M, i);
         T Rn[9], on[3], z[3];
         joint_pose<T>(J, R, o, i == 0, q[i], Rn, on, z);
         if (i > 0) {

@@ -16,6 +16,8 @@
 //                 LDS), solve, fraction to the boundary, line search (trial values: one lane per
 //                 node) with second-order corrections, update
 // Layout: every per-problem array is [problem][node][field]; a node's record is contiguous.
+// the phase kernels read their model images in LDS through generic pointers (dyn.hpp joint_at)
+#define MF_GENERIC_MODEL_PTR 1
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -165,6 +167,51 @@ __device__ unsigned long long mf_gstamp_buf[32 * 1024];
 #define GSTAMP_INIT do {} while (0)
 #define GSTAMP_COUNT(slot, v) do {} while (0)
 #define GSTAMP_FLUSH do {} while (0)
+#endif
+
+// Diagnostic build only (-DMF_GCHK, libmpcfatigue_gchk.so): progress checkpoints of the phase kernels and index
+// checks of the stored stage factorisations (0 <= perm < NK, piv in {0, 1, 2}), written by plain vector stores to
+// mapped host memory (mf_gdebug_chk_attach); if the runtime aborts the process on a GPU fault, a SIGABRT handler
+// writes that memory to a file.  Per problem b < GCHK_B four words: [0] (iter << 12) | (phase << 8) | checkpoint,
+// [1] violation flags (1 perm, 2 piv, 4 perm at the factorisation, 8 piv at the factorisation), [2] auxiliary
+// value (stage, trial), [3] the offending value.  Out-of-range indices are clamped in this build.
+#define GCHK_B 4096
+#define GCHK_W 68  // words per problem: the four above, then one per lane (GCHK_LANE)
+#ifdef MF_GCHK
+__device__ unsigned *mf_gchk_dev;
+__device__ __forceinline__ void gchk_store(unsigned *p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define GCHK(id, aux)                                                                                           \
+    do {                                                                                                        \
+        unsigned *g_ = mf_gchk_dev;                                                                             \
+        if (lane == 0 && g_ && b < GCHK_B) {                                                                    \
+            gchk_store(g_ + GCHK_W * b, ((unsigned)st.iter << 12) | ((unsigned)PH << 8) | (unsigned)(id));            \
+            gchk_store(g_ + GCHK_W * b + 2, (unsigned)(aux));                                                         \
+            __threadfence_system();                                                                             \
+        }                                                                                                       \
+    } while (0)
+#define GCHK_BAD(code, val)                                                                                     \
+    do {                                                                                                        \
+        unsigned *g_ = mf_gchk_dev;                                                                             \
+        if (g_ && b < GCHK_B) {                                                                                 \
+            gchk_store(g_ + GCHK_W * b + 1, (unsigned)(code));                                                        \
+            gchk_store(g_ + GCHK_W * b + 3, (unsigned)(val));                                                         \
+            __threadfence_system();                                                                             \
+        }                                                                                                       \
+    } while (0)
+#define GCHK_LANE(v)                                                                                            \
+    do {                                                                                                        \
+        unsigned *g_ = mf_gchk_dev;                                                                             \
+        if (g_ && b < GCHK_B) {                                                                                 \
+            gchk_store(g_ + GCHK_W * b + 4 + lane, (unsigned)(v));                                               \
+            __threadfence_system();                                                                             \
+        }                                                                                                       \
+    } while (0)
+#else
+#define GCHK(id, aux) do {} while (0)
+#define GCHK_BAD(code, val) do {} while (0)
+#define GCHK_LANE(v) do {} while (0)
 #endif
 
 // first NJ joints of a DevModel in LDS
@@ -419,10 +466,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     if (b >= batch) return;
     GState st = A.st[b];
     if (st.status != GS_RUNNING) return;
+    GCHK(1, 0);
     __shared__ GModels<FAM> Gm;
     if constexpr (PH == 2) {
         Gm.load(M0, M1, F0, F1);
         __syncthreads();
+        GCHK(2, 0);
     }
     // the LDS images' generic addresses made opaque: with many inlined users the optimiser otherwise folds the
     // {&Gm.m[0], &Gm.m[1]} aggregate into a constant global initialiser, which cannot hold LDS addresses
@@ -1103,6 +1152,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             // the stage factorisation is kept (the solves of the vector pass and of the second-order
             // corrections reuse it: a backward-stable LDL^T solve, not an explicit inverse)
             double *kst = Kg + (size_t)k * KSTG;
+#ifdef MF_GCHK
+            for (int e = lane; e < NK; e += 64) {
+                if (perm[e] < 0 || perm[e] >= NK) GCHK_BAD(4, perm[e]);
+                if (piv[e] < 0 || piv[e] > 2) GCHK_BAD(8, piv[e]);
+            }
+#endif
             for (int e = lane; e < NK * LDK; e += 64) kst[e] = Ks[e];
             for (int e = lane; e < NK; e += 64) { kst[NK * LDK + e] = perm[e]; kst[NK * LDK + NK + e] = piv[e]; }
             for (int e = lane; e < NK * NX; e += 64) Kf[e] = -Rh[e];
@@ -1157,8 +1212,13 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 for (int e = lane; e < NK; e += 64) {
                     perm[e] = (int)kst[NK * LDK + e];
                     piv[e] = (int)kst[NK * LDK + NK + e];
+#ifdef MF_GCHK
+                    if (perm[e] < 0 || perm[e] >= NK) { GCHK_BAD(1, perm[e]); perm[e] = e; }
+                    if (piv[e] < 0 || piv[e] > 2) { GCHK_BAD(2, piv[e]); piv[e] = 1; }
+#endif
                 }
             }
+            GCHK(21, k);
             for (int j = lane; j < NX; j += 64)
                 if (k == 0) Vs[V_LP + j] = 0.0;
             for (int ee = lane; ee < NEA; ee += 64)
@@ -1226,6 +1286,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             GSTAMP(24);
             if constexpr (NK <= 24 && PH == 1) bk_solve_cols<LDK, 1, NK>(Ks, perm, piv, duv, 1);  // (k_gls: register budget)
             else bk_solve_wave<LDK, 1>(Ks, NK, perm, piv, duv, 1, Ys);
+            GCHK(22, k);
             for (int a = lane; a < NK; a += 64) kvg[k * NK + a] = duv[a];
             GSTAMP(25);
             if (k > 0)
@@ -1239,6 +1300,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         }
         GSTAMP(26);
         // forward sweep
+        GCHK(23, 0);
         for (int j = lane; j < NX; j += 64) { dxs[j] = 0.0; dx[j] = 0.0; }
         for (int ee = lane; ee < NEA; ee += 64) dye[ee] = 0.0;  // state rows of node 0 (inactive)
         gsync();
@@ -1289,6 +1351,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             gsync();
         }
         GSTAMP(17);
+        GCHK(24, 0);
         // slack rows and bound multipliers
         for (int e = lane; e < N * NI; e += 64) {
             const int k = e / NI, q = e % NI, i = k * NIA + q;
@@ -1385,8 +1448,10 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         double fs = 0.0, t = 0.0, bar = 0.0, lin = 0.0;
         int bad = 0;
         const double *pe = cur ? prr : tpr, *ne_ = cur ? nrr : tnr;  // elastic variables of the point (rsm)
+        GCHK(40, cur);
         for (int k = lane; k < N; k += 64) {
             double l, ci[NIA], ce[NET], f[NX];
+            GCHK_LANE((k << 8) | 1);
             if (cur) {
                 const double *rk = R(k);
                 l = rk[D::O_L];
@@ -1395,20 +1460,43 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 for (int m = 0; m < NM; m++) ce[NE + m] = rk[D::O_CM + m];
                 for (int j = 0; j < NX; j++) f[j] = rk[D::O_F + j];
             } else {
+#ifdef MF_GCHK
+                {  // which operand of the node function faults
+                    volatile double sink;
+                    sink = xx[(size_t)k * NX];
+                    GCHK_LANE((k << 8) | 11);
+                    sink = uu[(size_t)k * NU + NU - 1];
+                    GCHK_LANE((k << 8) | 12);
+                    sink = lref[0];
+                    GCHK_LANE((k << 8) | 13);
+                    sink = P.fdir[0] + P.h;
+                    GCHK_LANE((k << 8) | 14);
+                    sink = M[0].g[2] + (double)M[0].n;
+                    GCHK_LANE((k << 8) | 15);
+                    sink = M[0].j[FAM::NJ - 1].m;
+                    GCHK_LANE((k << 8) | 16);
+                    sink = F[0].t[2] + (double)F[0].parent;
+                    GCHK_LANE((k << 8) | 17);
+                    (void)sink;
+                }
+#endif
                 FAM::values(M, F, P, xx + (size_t)k * NX, uu + (size_t)k * NU, lref, l, ci, ce, f);
             }
+            GCHK_LANE((k << 8) | 2);
             if (!rsm) fs += l;
             for (int j = 0; j < NX; j++) {
                 const double r = f[j] - xx[(k + 1) * NX + j];
                 t += fabs(r);
                 if (trd) trd[k * NX + j] = r;
             }
+            GCHK_LANE((k << 8) | 3);
             for (int q = 0; q < NI; q++) {
                 const int i = k * NIA + q;
                 const double r = cact(k, q) ? ci[q] - ss[i] + (rsm ? ne_[i] - pe[i] : 0.0) : 0.0;
                 t += fabs(r);
                 if (tri) tri[i] = r;
             }
+            GCHK_LANE((k << 8) | 4);
             const bool eo = eqon(k);
             for (int ee = 0; ee < NEA; ee++) {
                 const size_t rr = NRo + (size_t)k * NET + ee;
@@ -1422,7 +1510,9 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 t += fabs(r);
                 if (tre) tre[k * NET + NEA + m] = r;
             }
+            GCHK_LANE((k << 8) | 5);
         }
+        GCHK(41, cur);
         auto blog = [&](double v, double lo, double hi) __attribute__((always_inline)) {
             if (gb(lo)) { if (v - lo <= 0) bad = 1; else bar -= log(v - lo); }
             if (gb(hi)) { if (hi - v <= 0) bad = 1; else bar -= log(hi - v); }
@@ -1456,6 +1546,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         th = t;
         okp = bad == 0;
         gsync();
+        GCHK(42, cur);
     };
     auto trial = [&](double al) __attribute__((always_inline)) {
         for (int e = lane; e < (N + 1) * NX; e += 64) tx[e] = x[e] + al * dx[e];
@@ -1542,6 +1633,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         d1 = (tier == 1) ? reg : 0.0;
         dw = (tier == 2) ? reg : 0.0;
     }
+    GCHK(30, factor_ok);
     if (!factor_ok && !lsm) { finish(GS_INERTIA); return; }
     if (lsm) {
         dw_c = 0.0;
@@ -1856,10 +1948,13 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     return;
     }  // flt
     double ap, az;
+    GCHK(3, 0);
     ftb(ap, az);
     double phi0, th0;
     bool ok0;
+    GCHK(4, 0);
     merit(x, u, s, true, nullptr, nullptr, nullptr, phi0, th0, ok0);
+    GCHK(5, 0);
     double gdot = 0.0, pHp = 0.0;
     for (int k = lane; k < N; k += 64) {
         const double *rk = R(k);
@@ -1888,10 +1983,13 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     int soc_used = 0;
     for (int ls = 0; ls < 40; ls++) {
         GSTAMP(7);
+        GCHK(6, ls);
         trial(alpha);
         double ph, th;
         bool okk;
+        GCHK(7, ls);
         merit(tx, tu, ts, false, trdyn, trin, treq, ph, th, okk);
+        GCHK(8, ls);
         GSTAMP_COUNT(21, 1);
         GSTAMP(5);
         const double mt = ph + nu * th;
@@ -1905,14 +2003,19 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             gsync();
             for (int p = 0; p < P.max_soc; p++) {
                 GSTAMP_COUNT(22, 1);
+                GCHK(9, p);
                 dir_copy(true);
+                GCHK(10, p);
                 direction(sdyn, sin_, seq);
+                GCHK(11, p);
                 double aps, azs;
                 ftb(aps, azs);
                 trial(aps);
                 double phs, ths;
                 bool oks;
+                GCHK(12, p);
                 merit(tx, tu, ts, false, trdyn, trin, treq, phs, ths, oks);
+                GCHK(13, p);
                 const double ms = phs + nu * ths;
                 if (oks && isfinite(ms) && ms - m0 <= eta * a_soc * fmin(Dphi, 0.0) + slack_m) {
                     accepted = true;
@@ -1922,6 +2025,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                     break;
                 }
                 dir_copy(false);
+                GCHK(14, p);
                 if (!oks || ths > 0.99 * th_old) break;
                 th_old = ths;
                 for (int e = lane; e < N * NX; e += 64) sdyn[e] = aps * sdyn[e] + trdyn[e];
@@ -1942,6 +2046,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     }
     st.n_soc += soc_used;
     GSTAMP(6);
+    GCHK(15, 0);
     for (int e = lane; e < (N + 1) * NX; e += 64) x[e] += alpha * dx[e];
     for (int e = lane; e < N * NU; e += 64) u[e] += alpha * du[e];
     for (int e = lane; e < N * NIA; e += 64) { s[e] += alpha * ds[e]; yi[e] += alpha * dyi[e]; }
@@ -1969,6 +2074,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     }
     GSTAMP(7);
     GSTAMP_FLUSH;
+    GCHK(16, 0);
     if (lane == 0) {
         st.iter++;
         st.mu = mu;
@@ -2392,9 +2498,10 @@ struct GOwnStream {
     hipStream_t s = nullptr;
     ~GOwnStream() { if (s) { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); } }
 };
-int gh2d(GBuf &b, const double *h, size_t n) {
+int gh2d(GBuf &b, const double *h, size_t n, hipStream_t s = nullptr) {
     GHIPCHK(hipMalloc(&b.p, n * sizeof(double)));
-    GHIPCHK(hipMemcpy(b.p, h, n * sizeof(double), hipMemcpyHostToDevice));
+    if (s) GHIPCHK(hipMemcpyAsync(b.p, h, n * sizeof(double), hipMemcpyHostToDevice, s));
+    else GHIPCHK(hipMemcpy(b.p, h, n * sizeof(double), hipMemcpyHostToDevice));
     return MF_OK;
 }
 int galloc(GBuf &b, size_t n) {
@@ -2413,16 +2520,17 @@ extern "C" int mf_gsolve_batch(mf_gproblem *p, int batch, const double *x0, cons
     const int ws = p->nx + p->spec.N * (p->nu + p->nx);
     GBuf dx0, du0, dw0, dl, dw, dk, dob;
     GIBuf dst, dit;
-    if ((e = gh2d(dx0, x0, (size_t)p->nx * batch))) return e;
-    if (u0 && (e = gh2d(du0, u0, (size_t)p->nu * batch))) return e;
-    if (w0 && (e = gh2d(dw0, w0, (size_t)ws * batch))) return e;
-    if (line_ref && (e = gh2d(dl, line_ref, 2 * (size_t)batch))) return e;
+    // this call's own stream: uploads, solve and copies back are ordered on it, and synchronising it
+    // leaves other handles / streams of the device running
+    GOwnStream os;
+    GHIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
+    if ((e = gh2d(dx0, x0, (size_t)p->nx * batch, os.s))) return e;
+    if (u0 && (e = gh2d(du0, u0, (size_t)p->nu * batch, os.s))) return e;
+    if (w0 && (e = gh2d(dw0, w0, (size_t)ws * batch, os.s))) return e;
+    if (line_ref && (e = gh2d(dl, line_ref, 2 * (size_t)batch, os.s))) return e;
     if ((e = galloc(dw, (size_t)ws * batch)) || (e = galloc(dk, batch)) || (e = galloc(dob, batch))) return e;
     GHIPCHK(hipMalloc(&dst.p, sizeof(int) * batch));
     GHIPCHK(hipMalloc(&dit.p, sizeof(int) * batch));
-    // this call's own stream: synchronising it leaves other handles / streams of the device running
-    GOwnStream os;
-    GHIPCHK(hipStreamCreateWithFlags(&os.s, hipStreamNonBlocking));
     e = gdispatch_solve(p, batch, dx0.p, du0.p, dw0.p, line_ref ? dl.p : nullptr, opts, dw.p, dst.p, dit.p, dk.p,
                         dob.p, os.s);
     if (e) return e;
@@ -2503,6 +2611,48 @@ extern "C" int mf_gdebug_trace_reset(void) {
     GHIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(mf_gdbg_ls), z.data(), sizeof(double) * z.size()));
     return MF_OK;
 }
+
+#ifdef MF_GCHK
+// diagnostic build: the checkpoint words live in mapped host memory; the SIGABRT handler (the runtime aborts the
+// process on a GPU fault) and mf_gdebug_chk_dump write them to the file named at attach time
+#include <csignal>
+#include <fcntl.h>
+#include <unistd.h>
+namespace {
+unsigned *g_chk_host = nullptr;
+char g_chk_path[512];
+void gchk_write() {
+    const int fd = open(g_chk_path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) return;
+    const ssize_t n = write(fd, g_chk_host, sizeof(unsigned) * GCHK_W * GCHK_B);
+    (void)n;
+    close(fd);
+}
+void gchk_on_abort(int sig) {
+    if (g_chk_host) gchk_write();
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+}  // namespace
+extern "C" int mf_gdebug_chk_attach(const char *path) {
+    if (!path) return capi_fail(MF_ERR_ARG, "null path");
+    snprintf(g_chk_path, sizeof g_chk_path, "%s", path);
+    if (!g_chk_host) {
+        GHIPCHK(hipHostMalloc(reinterpret_cast<void **>(&g_chk_host), sizeof(unsigned) * GCHK_W * GCHK_B, hipHostMallocMapped));
+        unsigned *d = nullptr;
+        GHIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&d), g_chk_host, 0));
+        GHIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(mf::mf_gchk_dev), &d, sizeof d));
+        signal(SIGABRT, gchk_on_abort);
+    }
+    memset(g_chk_host, 0, sizeof(unsigned) * GCHK_W * GCHK_B);
+    return MF_OK;
+}
+extern "C" int mf_gdebug_chk_dump(void) {
+    if (!g_chk_host) return capi_fail(MF_ERR_ARG, "not attached");
+    gchk_write();
+    return MF_OK;
+}
+#endif
 
 extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {
     if (!p || !out) return capi_fail(MF_ERR_ARG, "null argument");

@@ -21,10 +21,11 @@ def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
 def gather_solutions(w, status, rank: int, world: int, dst: int = 0, total: int | None = None):
     """Gather every rank's solution block to `dst`; returns (W, S) on dst, (None, None) elsewhere.
 
-    Shards may differ in size by one horizon (shard_range of a total not divisible by world): every
-    rank pads its block to the largest shard (ceil(total / world) rows), the gather moves equal
-    blocks, and dst drops each rank's padding.  total defaults to world x this rank's rows (equal
-    shards, the bench's batch-per-GPU shards).
+    Shards may differ in size (shard_range of a total not divisible by world): the ranks first
+    all-gather their row counts, so every rank knows every block's size and the same total; each
+    rank pads its block to the largest one, the gather moves equal blocks, and dst drops the
+    padding.  If `total` is given and the gathered row counts do not match shard_range(total),
+    EVERY rank raises the same ValueError (no rank is left blocked in the gather).
     """
     import torch
     import torch.distributed as dist
@@ -32,10 +33,14 @@ def gather_solutions(w, status, rank: int, world: int, dst: int = 0, total: int 
     if world == 1:
         return w, status
     rows = w.shape[0]
-    total = rows * world if total is None else total
-    sizes = [shard_range(total, world, r)[1] - shard_range(total, world, r)[0] for r in range(world)]
-    if sizes[rank] != rows:
-        raise ValueError(f"rank {rank} holds {rows} rows, shard_range({total}, {world}) gives {sizes[rank]}")
+    cnt = torch.tensor([rows], dtype=torch.int64, device=w.device)
+    got = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(got, cnt)
+    sizes = [int(c.item()) for c in got]
+    if total is not None:
+        want = [shard_range(total, world, r)[1] - shard_range(total, world, r)[0] for r in range(world)]
+        if sizes != want:
+            raise ValueError(f"shard rows {sizes} do not match shard_range({total}, {world}) = {want}")
     m = max(sizes)
     if rows < m:
         w = torch.cat([w, w.new_zeros((m - rows,) + tuple(w.shape[1:]))])

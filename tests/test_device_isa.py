@@ -1,10 +1,12 @@
-"""Device-code guard (CPU): the gfx950 code objects inside libmpcfatigue.so contain no device function calls.
+"""Device-code guards (CPU) on the gfx950 code objects inside libmpcfatigue.so (read from the clang offload
+bundles of the shared object; no GPU needed):
 
-Every kernel is one inlined body: a non-inlined device call (s_swappc_b64) passes its LDS arrays as flat pointers
-and keeps its locals in a scratch stack frame.  The only GPU fault of round 3 came from exactly that (the
-generic solver's line-search kernel calling a register-array triangular solve the inliner had declined: an
-aperture violation), so the heavy device routines are __forceinline__ and this test keeps it so.
-The code objects are read from the clang offload bundles of the shared object (no GPU needed).
+* no device function calls (s_swappc_b64) and no dynamic stack: every kernel is one inlined body;
+* no flat access whose immediate offset spans a joint record: the generic solver's kernels read their model
+  images in LDS through generic (flat) pointers, and the aperture of a flat access is decided on its base
+  register.  A joint loop strength-reduced to `base - 400 k` plus a folded offset put that base below the LDS
+  aperture and faulted the line-search kernel (MEMORY_APERTURE_VIOLATION, rounds 3 and 4);
+  dyn.hpp joint_at keeps each joint's address a pointer of its own, and this test keeps it so.
 """
 import os
 import re
@@ -67,3 +69,28 @@ def test_no_dynamic_stack(tmp_path):
             checked += 1
             assert not re.search(r"\.uses_dynamic_stack:\s+true", k), m.group(1)
     assert checked > 0
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(OBJDUMP)), reason="library or llvm-objdump missing")
+def test_no_flat_offset_across_joint_records(tmp_path):
+    """In the generic solver's kernels (mf::k_g*) every flat load / store offset stays inside one joint record
+    (sizeof(DevJoint) = 400 bytes, model.hpp): a larger one means a joint address folded into the instruction
+    offset, with the base register below the model image (see the module docstring)."""
+    worst = {}
+    for i, o in enumerate(_gfx950_objects(LIB)):
+        f = tmp_path / f"co{i}.o"
+        f.write_bytes(o)
+        asm = subprocess.run([OBJDUMP, "-d", str(f)], capture_output=True, text=True, check=True).stdout
+        cur = None
+        for line in asm.split("\n"):
+            m = re.match(r"^[0-9a-f]+ <(.*)>:", line)
+            if m:
+                cur = m.group(1)
+                continue
+            if cur and re.search(r"\d+k_g", cur):
+                m = re.search(r"\bflat_(?:load|store)\w*\s.*?offset:(\d+)", line)
+                if m:
+                    worst[cur] = max(worst.get(cur, 0), int(m.group(1)))
+    assert worst, "no flat access found in the generic kernels"
+    bad = {k: v for k, v in worst.items() if v >= 400}
+    assert not bad, bad

@@ -264,3 +264,45 @@ def test_first_solve_on_a_non_blocking_stream():
     assert (outs[0]["status"] == 0).all()
     np.testing.assert_array_equal(outs[0]["iters"], outs[1]["iters"])
     np.testing.assert_array_equal(outs[0]["w"], outs[1]["w"])
+
+
+def test_c5_full_batch_every_horizon():
+    """The whole C5 batch the bench solves (8192 horizons, N = 100, seed 0): every horizon
+    converges, and on every horizon the solution satisfies the transcription of force_optimization_pilz_6DOF.py
+    (L129-172) checked through the GPU bridge functions -- Euler continuity, the line x, y of prbt_link_5 at the
+    horizon's reference for k = 2..N-1 (k = 0, 1 are fixed data), and every node torque tau = ID(q, qd, 0) - J^T [F; 0]
+    inside the fatigue bound table (bound_relax 0).  64 horizons spread over the batch equal the oracle's solves
+    (q to 1e-6 rad, same status)."""
+    from mpc_fatigue_amd import pin
+    N, B = 100, 8192
+    base = PR.pilz6_bench(N=N)
+    ocp = OCP(base)
+    ref = load_urdf_file(PR.urdf_path(base["urdf"]))
+    Q0 = PR.pilz6_batch_q0(B, seed=0)
+    urdf = open(PR.urdf_path(base["urdf"])).read()
+    fk = pin.generate_forward_kin(urdf, "prbt_link_5")
+    LR = fk.batch(Q0)[0][:, :2]
+    res = ocp.solve(Q0, line_ref=LR, F_init=PR.BENCH_F_INIT, tol=1e-8, constr_viol_tol=1e-8, max_iter=300)
+    assert (res.status == 0).all(), np.flatnonzero(res.status != 0)[:10]
+    n, h = 6, base["h"]
+    blk = res.w[:, n:].reshape(B, N, 2 * n + 1)
+    q = np.concatenate([res.w[:, None, :n], blk[:, :, n + 1:]], axis=1)  # (B, N+1, 6)
+    qd, F = blk[:, :, :n], blk[:, :, n]
+    assert np.abs(q[:, 1:] - (q[:, :-1] + h * qd)).max() <= 1e-10
+    p = fk.batch(q[:, 2:N].reshape(-1, n))[0].reshape(B, N - 2, 3)  # line rows k = 2..N-1 (LINE_ON)
+    assert np.abs(p[:, :, :2] - LR[:, None, :]).max() <= 1e-8
+    idyn = pin.generate_inv_dyn(urdf)
+    jac = pin.generate_jacobian(urdf, "prbt_link_5")
+    qn, qdn = q[:, :N].reshape(-1, n), qd.reshape(-1, n)
+    tau = idyn.batch(qn, qdn, np.zeros_like(qn)) - jac.batch(qn)[:, 0, :] * F.reshape(-1, 1)
+    tau = tau.reshape(B, N, n)
+    lo, hi = np.asarray(base["tau_lo"]), np.asarray(base["tau_hi"])
+    assert (tau <= hi[None] + 1e-8).all() and (tau >= lo[None] - 1e-8).all()
+    idx = np.linspace(0, B - 1, 64).astype(int)
+    specs = [PR.pilz6_bench(N=N, q0=Q0[b], line_ref=LR[b]) for b in idx]
+    W, R = O.solve_batch(ref, specs, F_init=PR.BENCH_F_INIT, tol=1e-8, constr_viol_tol=1e-8, max_iter=300)
+    worst = 0.0
+    for i, b in enumerate(idx):
+        assert R[i].status == 0
+        worst = max(worst, np.abs(ocp.unpack(res.w[b])[0] - ocp.unpack(W[i])[0]).max())
+    assert worst <= 1e-6, worst

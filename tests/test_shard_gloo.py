@@ -29,25 +29,30 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, total):
+def _worker(rank, world, port, q, total, pass_total=True, claim=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard_range(total, world, rank)
     w = torch.arange(lo * 5, hi * 5, dtype=torch.float64).reshape(hi - lo, 5)
     st = torch.full((hi - lo,), rank, dtype=torch.int32)
-    W, S = gather_solutions(w, st, rank, world, total=total)
-    if rank == 0:
-        q.put((W.numpy().tolist(), S.numpy().tolist()))
+    try:
+        W, S = gather_solutions(w, st, rank, world, total=(claim or total) if pass_total else None)
+    except ValueError as e:
+        q.put(("error", rank, str(e)))
+    else:
+        if rank == 0:
+            q.put((W.numpy().tolist(), S.numpy().tolist()))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total", [(2, 16), (2, 17)])
-def test_gather_solutions_gloo(world, total):
-    """Equal shards and unequal ones (17 horizons over 2 ranks: 9 + 8, padded for the gather)."""
+@pytest.mark.parametrize("world,total,pass_total", [(2, 16, True), (2, 17, True), (2, 17, False)])
+def test_gather_solutions_gloo(world, total, pass_total):
+    """Equal shards and unequal ones (17 horizons over 2 ranks: 9 + 8, padded for the gather), with the
+    total given or left to the collective row-count agreement."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, total)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, total, pass_total)) for r in range(world)]
     for p in procs:
         p.start()
     W, S = q.get(timeout=120)
@@ -60,6 +65,21 @@ def test_gather_solutions_gloo(world, total):
     np.testing.assert_array_equal(W.reshape(-1), np.arange(total * 5))
     spans = [shard_range(total, world, r) for r in range(world)]
     assert S == [r for r in range(world) for _ in range(spans[r][1] - spans[r][0])]
+
+
+def test_gather_solutions_mismatch_fails_on_every_rank():
+    """A total that disagrees with the shards held raises on every rank (none is left in the gather)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, 17, True, 18)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120)[:2] for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [("error", 0), ("error", 1)]
 
 
 def _solve_worker(rank, world, port, q):
