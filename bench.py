@@ -10,6 +10,7 @@ gives C5's 8-GPU shard size).  value = horizons that reached the KKT tolerance o
 all ranks / max-over-ranks wall time (inputs resident in HBM).
 
     python bench.py [--gpus N --steps K --warmup W --batch B --nodes 100]
+    python bench.py --c5 ...   (C5 as SURVEY.md s.8(e): --batch horizons in total, sharded; strong scaling)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Also reported: the node-evaluation kernel's achieved rate against its HBM
@@ -115,6 +116,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=8192,
                     help="horizons per GPU (default: the C5 batch of 8192 on every GPU, weak scaling)")
+    ap.add_argument("--c5", action="store_true",
+                    help="BASELINE config C5 as SURVEY.md s.8(e) defines it: --batch horizons IN TOTAL (default 8192), "
+                         "sharded over the ranks by shard_range (1024 per GPU at N = 8; strong scaling)")
     ap.add_argument("--nodes", type=int, default=100)
     ap.add_argument("--max-iter", type=int, default=300)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,12 +159,13 @@ def main() -> int:
     from mpc_fatigue_amd.ocp import OCP
     from mpc_fatigue_amd.shard import shard_range, gather_solutions
 
-    N, B = args.nodes, args.batch
+    N = args.nodes
     spec = PR.pilz6_bench(N=N)
     ocp = OCP(spec)
     n = ocp.n
-    gB = B * world
+    gB = args.batch if args.c5 else args.batch * world  # C5: a fixed total; default: --batch per GPU
     lo, hi = shard_range(gB, world, rank)
+    B = hi - lo
     Q0_all = PR.pilz6_batch_q0(gB, seed=0)
     q0 = torch.tensor(Q0_all[lo:hi], dtype=torch.float64, device=dev).contiguous()
     lref = torch.empty((hi - lo, 2), dtype=torch.float64, device=dev)
@@ -213,7 +218,7 @@ def main() -> int:
                     if world > 1 and nb == hi - lo:
                         i = (s_ - inflight) % inflight
                         _, _, ob, _ = slots[i]
-                        gather_solutions(ob["w"], ob["status"], rank, world)
+                        gather_solutions(ob["w"], ob["status"], rank, world, total=gB)
                         ev = torch.cuda.Event()
                         ev.record(torch.cuda.current_stream(dev))  # the stream the gather ran on
                         gathered[i] = ev
@@ -320,8 +325,9 @@ def main() -> int:
     result = {
         "metric": METRIC, "value": value, "unit": "horizons/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": f"pilz6_force N={N} (fatigue floor {PR.BENCH_FLOOR:g} Nm), {B} horizons per GPU, "
+        "scaling": "strong" if args.c5 else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": (f"C5: {gB} horizons in total over {world} GPU(s), " if args.c5 else "") +
+                               f"pilz6_force N={N} (fatigue floor {PR.BENCH_FLOOR:g} Nm), {B} horizons per GPU, "
                                "q0 = IK + U(-0.05,0.05), line ref = fk(q0)",
                    "horizon_nodes": N, "batch_per_gpu": B, "global_batch": gB,
                    "parallelism": f"dp{world} (independent horizons; RCCL gather of solutions)",
@@ -376,10 +382,11 @@ def main() -> int:
         # BASELINE configs 3 (dual-arm shared fatigue budget, N = 100) and 4 (Centauro, N = 50) through the
         # generic stage-structured solver (csrc/gipm.hip): batches of perturbed starts, GPU vs the host IPM
         sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from generic_bench import GENERIC_STAGE_CAPS, generic_extra
+        from generic_bench import generic_extra
         torch.cuda.set_device(dev)
+        # IPOPT mode (the reference's solve: x0 = 0, filter globalisation, bound_relax 1e-8; no homotopy)
         result["generic"] = generic_extra(batch=args.generic_batch, sample=2, cpu=not args.no_cpu_baseline,
-                                          stage_caps=GENERIC_STAGE_CAPS)
+                                          mode="ipopt")
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import pin_np as P

@@ -2120,7 +2120,7 @@ __global__ void k_gout(GArrays A, int N, int batch, double *w, int *status, int 
     }
     if (lane == 0) {
         const GState st = A.st[b];
-        if (status) status[b] = st.status;
+        if (status) status[b] = st.status == GS_RUNNING ? GS_MAXITER : st.status;  // (host launch bound reached)
         if (iters) iters[b] = st.iter;
         if (kkt) kkt[b] = st.E0;
         if (obj) obj[b] = st.obj;
@@ -2320,7 +2320,11 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     const int rec_blocks = (int)(((long)batch * P.N + 3) / 4);
     int active = batch;
     const int chunk = 4;
-    for (int it = 0; it <= P.max_iter && active > 0; it += chunk) {
+    // every running horizon ends at the latest when its own iteration count reaches max_iter; in IPOPT mode
+    // some launches advance no iteration (the restoration phase's start and end), so the host bound is on
+    // launches, with room for those, not on iterations
+    const int max_launches = 2 * P.max_iter + 64;
+    for (int it = 0; it < max_launches && active > 0; it += chunk) {
         for (int c = 0; c < chunk; c++) {
             hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
             hipLaunchKernelGGL(k_gasm<FAM>, dim3(rec_blocks), dim3(256), 0, s, P, A, batch);
