@@ -118,7 +118,14 @@ def restart_state(w, nx: int, nu: int, N: int, n: int, thermal: bool, T_drop: fl
 
 class GRecedingHorizon:
     """Repeated solves of a generic problem (gocp.GOCP) for a batch of initial states, restarted
-    as mpc_principal.py:357-377 restarts the Centauro MPC."""
+    as mpc_principal.py:357-377 restarts the Centauro MPC.
+
+    The first solve differs between the reference's two Centauro loops:
+      * RepeatedMPCwithThermal.py:445-448, 464-466: cold -- no x0 (IPOPT from 0, the `x0=sol0` call is
+        commented out at L465) and no warm_start_init_point; run(x0, ...) with w0=None.
+      * mpc_principal.py:348-351, 357-360: warm_start_init_point = yes already at s = 0, from x0 = sol0;
+        run(x0, ..., w0=sol0, warm_first=True).
+    From the second solve on both warm-start from the previous solution (L446 / L349)."""
 
     def __init__(self, spec: dict, carry_velocity: bool = True, T_drop: float = 0.05, decimals: int | None = 4,
                  models=None, restart_spec: dict | None = None, warm_start: bool = True, **opts):
@@ -141,8 +148,10 @@ class GRecedingHorizon:
         return restart_state(w, g.nx, g.nu, g.N, self.n, self.thermal, self.T_drop, self.carry_velocity,
                              self.decimals)
 
-    def run(self, x0, steps: int, u0=None, line_ref=None, device: int = 0) -> list:
-        """Device-resident loop; returns the per-step SolveResults (host copies)."""
+    def run(self, x0, steps: int, u0=None, line_ref=None, device: int = 0, w0=None, warm_first: bool = False) -> list:
+        """Device-resident loop; returns the per-step SolveResults (host copies).  w0: the first solve's start
+        (the reference's sol0, B x wsize or one row for every problem); warm_first: that solve with IPOPT's
+        warm_start_init_point constants (mpc_principal.py:349-351) instead of the cold initial point."""
         import torch
 
         g = self.g
@@ -160,6 +169,9 @@ class GRecedingHorizon:
                "obj": torch.empty(B, dtype=torch.float64, device=dev)}
         stream = torch.cuda.current_stream(dev).cuda_stream
         res, prev = [], None
+        if w0 is not None:
+            prev = torch.as_tensor(np.broadcast_to(np.asarray(w0, float), (B, g.wsize)).copy(), dtype=torch.float64,
+                                   device=dev).contiguous()
         for s in range(steps):
             w = wbuf[s % 2]
             ptr = {k: v.data_ptr() for k, v in out.items()}
@@ -167,7 +179,7 @@ class GRecedingHorizon:
             (g if s == 0 else self.g_restart).solve_dev(
                 x.data_ptr(), None if u is None else u.data_ptr(), None if prev is None else prev.data_ptr(),
                 None if lr is None else lr.data_ptr(), B, ptr, stream=stream,
-                warm_start=self.warm_start and prev is not None, **self.opts)
+                warm_start=(self.warm_start and s > 0) or (warm_first and s == 0 and prev is not None), **self.opts)
             res.append(SolveResult(w.cpu().numpy(), out["status"].cpu().numpy(), out["iters"].cpu().numpy(),
                                    out["kkt"].cpu().numpy(), out["obj"].cpu().numpy()))
             x, u = self.next_initial(w)

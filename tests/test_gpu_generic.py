@@ -287,6 +287,29 @@ def test_centauro_receding_horizon_gpu_matches_oracle():
     assert x[14:].max() > 20.5
 
 
+def test_centauro_mpc_principal_warm_first_solve_matches_oracle():
+    """mpc_principal.py:348-360 starts its loop with warm_start_init_point already at s = 0, from x0 = sol0
+    (RepeatedMPCwithThermal.py runs that solve cold): GRecedingHorizon.run(w0=sol0, warm_first=True) on the
+    GPU equals the oracle's warm-started solve from the same sol0 (the reference's held state, each hand
+    carrying half the box), step 0 and the first restart."""
+    from mpc_fatigue_amd.mpc import GRecedingHorizon
+
+    N = 20
+    spec = PR.centauro(N=N)
+    kw = dict(tol=1e-3, constr_viol_tol=1e-3, max_iter=500, max_soc=4)
+    g, _ = G.make(spec)
+    nx, nu = g.nx, g.nu
+    x0 = np.r_[spec["q0"], spec["T0"]]
+    sol0 = np.r_[x0, np.tile(np.r_[PR.centauro_u_init(spec), x0], N)]  # sol0: held state, F = (0, 0, mg/2)
+    loop = GRecedingHorizon(spec, restart_spec=dict(spec, target_decimals=3), **kw)
+    res = loop.run(x0[None], 2, w0=sol0, warm_first=True)
+    w, r = G.solve(spec, w0=sol0, warm_start=True, **kw)
+    assert int(res[0].status[0]) == r.status == 0, (int(res[0].status[0]), r.status)
+    np.testing.assert_allclose(res[0].w[0], w, atol=1e-6)
+    assert abs(int(res[0].iters[0]) - r.iter) <= 2
+    assert int(res[1].status[0]) == 0
+
+
 def test_box_shared_fatigue_gpu_matches_oracle(golden):
     """C3 at N = 100 with the shared fatigue budget (BASELINE config 3; build-defined, parity against the
     oracle only): the winding temperatures of all 12 joints as state, one budget row per node.  IPOPT mode (the

@@ -46,7 +46,10 @@ def _x_traj(w, nx, nu, N):
     return np.concatenate([w[:, None, :nx], w[:, nx:].reshape(w.shape[0], N, nu + nx)[:, :, nu:]], axis=1)
 
 
-IPOPT_KW = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=1500, max_soc=4)
+# IPOPT at the reference's settings: no option is set in Box_Pilz_6DOF.py:455 / RepeatedMPCwithThermal.py:466, so
+# max_iter is IPOPT's default 3000 (the filter path of a few starts is long: r04, 2 of 512 C3 starts need more than
+# 1500 iterations on the device, 5 others on the host IPM -- round-off-sensitive restoration exits)
+IPOPT_KW = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=3000, max_soc=4)
 
 
 def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0, cases=("c3", "c4"),

@@ -18,6 +18,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--cases", default="c3,c4")
+    ap.add_argument("--max-iter", type=int, default=0, help="override IPOPT_KW's max_iter")
     a = ap.parse_args()
     from generic_bench import IPOPT_KW, _golden_q0
     from mpc_fatigue_amd import problems as PR
@@ -32,9 +33,10 @@ if __name__ == "__main__":
     for case, spec, X in (("c3", sp3, X3), ("c4", sp4, X4)):
         if case not in a.cases:
             continue
-        r = GOCP(spec).solve(x0=X, **IPOPT_KW)
+        kw = dict(IPOPT_KW, **({"max_iter": a.max_iter} if a.max_iter else {}))
+        r = GOCP(spec).solve(x0=X, **kw)
         st = np.asarray(r.status)
         vals, cnt = np.unique(st, return_counts=True)
         print(case, dict(zip(vals.tolist(), cnt.tolist())), "mean iters", float(np.mean(r.iters)), flush=True)
-        np.savez(os.path.join(ROOT, "gpurun_out", f"ipopt_fail_{case}.npz"), X=X, status=st, iters=np.asarray(r.iters),
+        np.savez(os.path.join(ROOT, "gpurun_out", f"ipopt_fail_{case}{'_' + str(a.max_iter) if a.max_iter else ''}.npz"), X=X, status=st, iters=np.asarray(r.iters),
                  obj=np.asarray(r.obj), kkt=np.asarray(r.kkt), w=np.asarray(r.w))
