@@ -248,6 +248,14 @@ int mf_gsolve_batch(mf_gproblem *p, int batch, const double *x0, const double *u
 int mf_gsolve_batch_dev(mf_gproblem *p, int batch, const double *x0, const double *u0, const double *w0,
                         const double *line_ref, const mf_gopts *opts, double *w, int *status, int *iters,
                         double *kkt, double *obj, void *stream);
+/* Continuous batching (device memory, build-defined: the reference solves one problem per nlpsol call,
+ * Box_Pilz_6DOF.py:455-456, RepeatedMPCwithThermal.py:466): `slots` solves run at once and work through
+ * `total` independent problems -- a slot whose problem has finished is handed the next one, so a few long
+ * solves do not hold the device at single-problem latency.  Inputs and outputs have `total` rows; every
+ * problem's result equals mf_gsolve_batch_dev's for the same row. */
+int mf_gsolve_stream_dev(mf_gproblem *p, int total, int slots, const double *x0, const double *u0, const double *w0,
+                         const double *line_ref, const mf_gopts *opts, double *w, int *status, int *iters,
+                         double *kkt, double *obj, void *stream);
 /* One node record evaluated by the device kernel (tests): xu = [x | u], multipliers yi (ni), ye (ne),
  * lam (nx); rec = [l | grad l (nv) | c_in (ni) | d c_in (ni x nv) | c_eq (ne) | d c_eq / dx (ne x nx) |
  * f (nx) | A (nx x nx) | B (nx x nu) | W (nv x nv)], row-major blocks.  Returns the record size. */

@@ -126,6 +126,8 @@ def lib() -> C.CDLL:
         "mf_gproblem_dims": ([vp, ip], C.c_int),
         "mf_gsolve_batch": ([vp, C.c_int, dp, dp, dp, dp, C.POINTER(GOpts), dp, ip, ip, dp, dp, C.c_int], C.c_int),
         "mf_gsolve_batch_dev": ([vp, C.c_int, vp, vp, vp, vp, C.POINTER(GOpts), vp, vp, vp, vp, vp, vp], C.c_int),
+        "mf_gsolve_stream_dev": ([vp, C.c_int, C.c_int, vp, vp, vp, vp, C.POINTER(GOpts), vp, vp, vp, vp, vp, vp],
+                                 C.c_int),
         "mf_gnode_record": ([vp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
         "mf_gdebug_duals": ([vp, C.c_int, dp], C.c_int),
         "mf_gdebug_trace": ([dp], C.c_int),
@@ -147,6 +149,7 @@ EXPORTED_SYMBOLS = [
     "mf_solve_batch_ws_dev", "mf_problem_timing",
     "mf_problem_kernel_stats", "mf_problem_trace", "mf_kernel_name", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
     "mf_gproblem_create", "mf_gproblem_free", "mf_gproblem_dims", "mf_gsolve_batch", "mf_gsolve_batch_dev",
+    "mf_gsolve_stream_dev",
     "mf_gnode_record", "mf_gdebug_duals", "mf_gdebug_trace", "mf_gdebug_trace_reset",
 ]
 

@@ -84,6 +84,14 @@ struct GArrays {
     // condensed Sigma / barrier gradients / residual corrections, and the reference point w_R, D_R^2
     double *fil, *wdit, *wddir;
     double *pr, *nr, *zp, *zn, *dpr, *dnr, *dzp, *dzn, *tpr, *tnr, *Sp, *Sn, *gp, *gn, *rowr, *wR, *dR;
+    // continuous batching (mf_gsolve_stream_dev): slot b holds problem pidx[b] (-1: none); k_gharvest writes a
+    // finished slot's result to its problem's output row and hands the slot the next unsolved problem, which
+    // k_ginit then initialises (init[b] = 1).  pidx == nullptr: slot b is problem b (mf_gsolve_batch*).
+    int *pidx, *next, *init;
+    int total;
+    const double *x0all, *lrall;  // every problem's x_0 and line reference (total rows)
+    double *ow, *okkt, *oobj;     // every problem's outputs
+    int *ost, *oit;
 };
 
 template <class D> struct GSz {
@@ -376,9 +384,11 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
                                               const DevFrame *F1, GParams P, GArrays A, int batch) {
     using D = typename FAM::D;
     constexpr int NX = D::NX, NU = D::NU, NI = D::NI, NIA = D::NIA, NET = D::NET;
+    if (blockIdx.x >= (unsigned)batch) return;
+    if (A.init && !A.init[blockIdx.x]) return;  // continuous batching: only the slots handed a new problem
     GMODELS(FAM);
     const int b = blockIdx.x, lane = threadIdx.x;
-    if (b >= batch) return;
+    const int pb = A.pidx ? A.pidx[b] : b;  // the problem in this slot (its u_0 / warm-start rows)
     const int N = P.N;
     const GSz<D> Z(N);
     double *x = A.x + b * Z.x(), *u = A.u + b * Z.u(), *s = A.s + b * Z.i();
@@ -388,7 +398,7 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         gsync();
     }
     const int wst = NU + NX, wsz = NX + N * wst;
-    const double *w0 = A.w0 ? A.w0 + (size_t)b * wsz : nullptr;
+    const double *w0 = A.w0 ? A.w0 + (size_t)pb * wsz : nullptr;
     // IPOPT initial point: bound_push = bound_frac = 1e-2 and bound multipliers 1 (bound_mult_init_val);
     // warm_start_init_point: 1e-3 and warm_start_mult_bound_push = 1e-3 (oracle/mf_ocp.c, same rule)
     const bool warm = P.warm_start && w0;
@@ -408,7 +418,7 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         const bool fixed = gb(lo) && lo == hi;
         double v;
         if (fixed) {
-            v = (k == 0 && A.u0) ? A.u0[(size_t)b * NU + j] : lo;
+            v = (k == 0 && A.u0) ? A.u0[(size_t)pb * NU + j] : lo;
         } else {
             double v0 = P.has_u_init ? P.u_init[j] : (j >= P.force_from ? P.F_init : 0.0);
             if (w0) v0 = w0[NX + k * wst + j];
@@ -445,6 +455,7 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         st.mode = 0; st.pend = GP_NONE; st.nf[0] = st.nf[1] = 0;
         st.in_wd = st.wd_short = st.wd_trial = st.in_soft = st.soft_cnt = st.n_resto = st.n_wd = st.n_soft = 0;
         A.st[b] = st;
+        if (A.init) A.init[b] = 0;
     }
 }
 
@@ -2127,6 +2138,56 @@ __global__ void k_gout(GArrays A, int N, int batch, double *w, int *status, int 
     }
 }
 
+// Continuous batching: a finished slot's solution goes to its problem's output row, and the slot takes the next
+// unsolved problem (x_0 and line reference staged into the slot; k_ginit initialises it).  force: the host's
+// launch bound was reached -- running slots are written out as max_iter and no problem is handed out.
+template <class FAM>
+__global__ __launch_bounds__(64) void k_gharvest(GArrays A, int N, int batch, int force) {
+    using D = typename FAM::D;
+    constexpr int NX = D::NX, NU = D::NU;
+    const int b = blockIdx.x, lane = threadIdx.x;
+    if (b >= batch) return;
+    const int pb = A.pidx[b];
+    if (pb < 0) return;
+    const GState st = A.st[b];
+    if (st.status == GS_RUNNING && !force) return;
+    const GSz<D> Z(N);
+    const int ws = NX + N * (NU + NX);
+    const double *x = A.x + b * Z.x(), *u = A.u + b * Z.u();
+    double *wb = A.ow + (size_t)pb * ws;
+    for (int e = lane; e < ws; e += 64) {
+        double v;
+        if (e < NX) v = x[e];
+        else {
+            const int k = (e - NX) / (NU + NX), r = (e - NX) % (NU + NX);
+            v = r < NU ? u[k * NU + r] : x[(k + 1) * NX + r - NU];
+        }
+        wb[e] = v;
+    }
+    int q = A.total;
+    if (lane == 0) {
+        if (A.ost) A.ost[pb] = st.status == GS_RUNNING ? GS_MAXITER : st.status;
+        if (A.oit) A.oit[pb] = st.iter;
+        if (A.okkt) A.okkt[pb] = st.E0;
+        if (A.oobj) A.oobj[pb] = st.obj;
+        if (st.status == GS_RUNNING) atomicSub(A.active, 1);
+        if (!force) q = atomicAdd(A.next, 1);
+    }
+    q = __shfl(q, 0, 64);
+    if (q < A.total) {
+        for (int j = lane; j < NX; j += 64) A.x0[(size_t)b * NX + j] = A.x0all[(size_t)q * NX + j];
+        if (FAM::LREF == 2 && A.lrall)
+            for (int j = lane; j < 2; j += 64) A.lref[2 * (size_t)b + j] = A.lrall[2 * (size_t)q + j];
+        if (lane == 0) {
+            A.pidx[b] = q;
+            A.init[b] = 1;
+            atomicAdd(A.active, 1);
+        }
+    } else if (lane == 0) {
+        A.pidx[b] = -1;
+    }
+}
+
 // single node record for tests (batch of one node, multipliers given)
 template <class FAM>
 __global__ __launch_bounds__(256) void k_grec(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
@@ -2185,6 +2246,7 @@ struct mf_gproblem {
     GArrays A;
     GState *d_st = nullptr;
     int *d_active = nullptr;
+    int *d_slots = nullptr;  // continuous batching: pidx (cap) | init (cap) | next (1)
 };
 
 template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **, size_t>> &items, GArrays &A) {
@@ -2213,8 +2275,10 @@ static void gfree_ws(mf_gproblem *p) {
     p->bufs.clear();
     if (p->d_st) (void)hipFree(p->d_st);
     if (p->d_active) (void)hipFree(p->d_active);
+    if (p->d_slots) (void)hipFree(p->d_slots);
     p->d_st = nullptr;
     p->d_active = nullptr;
+    p->d_slots = nullptr;
     p->cap = 0;
 }
 
@@ -2238,6 +2302,7 @@ template <class FAM> static int gensure_ws(mf_gproblem *p, int batch, hipStream_
     }
     GHIPCHK(hipMalloc(&p->d_st, sizeof(GState) * (size_t)batch));
     GHIPCHK(hipMalloc(&p->d_active, sizeof(int)));
+    GHIPCHK(hipMalloc(&p->d_slots, sizeof(int) * (2 * (size_t)batch + 1)));
     A.st = p->d_st;
     A.active = p->d_active;
     A.u_lo = p->d_ulo;
@@ -2251,8 +2316,12 @@ template <class FAM> static int gensure_ws(mf_gproblem *p, int batch, hipStream_
 template <class FAM>
 static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const double *d_u0, const double *d_w0,
                        const double *d_lref, const mf_gopts *o, double *d_w, int *d_status, int *d_iters,
-                       double *d_kkt, double *d_obj, hipStream_t s) {
+                       double *d_kkt, double *d_obj, hipStream_t s, int total = 0) {
     using D = typename FAM::D;
+    // total > batch: continuous batching -- `batch` slots work through `total` problems (input and output
+    // arrays have `total` rows); a slot whose problem finished takes the next one (k_gharvest)
+    const bool stream_mode = total > batch;
+    if (!stream_mode) total = batch;
     int e = gensure_ws<FAM>(p, batch, s);
     if (e) return e;
     GParams P = p->P;
@@ -2298,6 +2367,21 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     A.u0 = d_u0;
     A.w0 = d_w0;
     A.u_lo = ulo; A.u_hi = uhi; A.c_lo = clo; A.c_hi = chi;
+    A.pidx = A.next = A.init = nullptr;
+    A.total = total;
+    A.x0all = d_x0;
+    A.lrall = FAM::LREF == 2 ? d_lref : nullptr;
+    A.ow = d_w; A.okkt = d_kkt; A.oobj = d_obj; A.ost = d_status; A.oit = d_iters;
+    if (stream_mode) {
+        std::vector<int> h(2 * (size_t)batch + 1, 0);
+        for (int b = 0; b < batch; b++) h[b] = b;  // slot b starts on problem b
+        h[2 * (size_t)batch] = batch;               // the next problem to hand out
+        GHIPCHK(hipMemcpyAsync(p->d_slots, h.data(), sizeof(int) * h.size(), hipMemcpyHostToDevice, s));
+        GHIPCHK(hipStreamSynchronize(s));
+        A.pidx = p->d_slots;
+        A.init = p->d_slots + batch;
+        A.next = p->d_slots + 2 * batch;
+    }
     GHIPCHK(hipMemcpyAsync(A.x0, d_x0, sizeof(double) * D::NX * (size_t)batch, hipMemcpyDeviceToDevice, s));
     if (FAM::LREF != 2) {
         // per-problem data computed by k_ginit from x_0
@@ -2313,7 +2397,11 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     GHIPCHK(hipStreamSynchronize(s));
     const DevModel *M0 = p->dM0, *M1 = p->dM1 ? p->dM1 : p->dM0;
     const DevFrame *F0 = p->dF0, *F1 = p->dF1 ? p->dF1 : p->dF0;
-    hipLaunchKernelGGL(k_ginit<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+    {
+        GArrays A0 = A;
+        A0.init = nullptr;  // the first launch initialises every slot
+        hipLaunchKernelGGL(k_ginit<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A0, batch);
+    }
     GHIPCHK(hipGetLastError());
     constexpr int NPB = 256 / FAM::LANES;
     const int eval_blocks = (int)(((long)batch * P.N + NPB - 1) / NPB);
@@ -2323,8 +2411,8 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     // every running horizon ends at the latest when its own iteration count reaches max_iter; in IPOPT mode
     // some launches advance no iteration (the restoration phase's start and end), so the host bound is on
     // launches, with room for those, not on iterations
-    const int max_launches = 2 * P.max_iter + 64;
-    for (int it = 0; it < max_launches && active > 0; it += chunk) {
+    const long max_launches = (2L * P.max_iter + 64) * (stream_mode ? (total + batch - 1) / batch + 1 : 1);
+    for (long it = 0; it < max_launches && active > 0; it += chunk) {
         for (int c = 0; c < chunk; c++) {
             hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
             hipLaunchKernelGGL(k_gasm<FAM>, dim3(rec_blocks), dim3(256), 0, s, P, A, batch);
@@ -2336,24 +2424,36 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
         GHIPCHK(hipGetLastError());
         GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
         GHIPCHK(hipStreamSynchronize(s));
-        if (o && o->verbose) fprintf(stderr, "[mf gipm] after %d iterations: %d running\n", it + chunk, active);
+        if (stream_mode && active < batch) {  // finished slots: outputs written, next problems handed out
+            hipLaunchKernelGGL(k_gharvest<FAM>, dim3(batch), dim3(64), 0, s, A, P.N, batch, 0);
+            hipLaunchKernelGGL(k_ginit<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            GHIPCHK(hipGetLastError());
+            GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
+            GHIPCHK(hipStreamSynchronize(s));
+        }
+        if (o && o->verbose) fprintf(stderr, "[mf gipm] after %ld launches: %d running\n", it + chunk, active);
     }
-    hipLaunchKernelGGL(k_gout<D>, dim3(batch), dim3(256), 0, s, A, P.N, batch, d_w, d_status, d_iters, d_kkt, d_obj);
+    if (stream_mode) {  // launch bound reached with slots still running: written out as max_iter
+        hipLaunchKernelGGL(k_gharvest<FAM>, dim3(batch), dim3(64), 0, s, A, P.N, batch, 1);
+    } else {
+        hipLaunchKernelGGL(k_gout<D>, dim3(batch), dim3(256), 0, s, A, P.N, batch, d_w, d_status, d_iters, d_kkt,
+                           d_obj);
+    }
     GHIPCHK(hipGetLastError());
     return MF_OK;
 }
 
 static int gdispatch_solve(mf_gproblem *p, int batch, const double *x0, const double *u0, const double *w0,
                            const double *lref, const mf_gopts *o, double *w, int *st, int *it, double *kkt,
-                           double *obj, hipStream_t s) {
+                           double *obj, hipStream_t s, int total = 0) {
     switch (p->kind) {
-        case GK_BOX: return gsolve_core<FamBox>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
-        case GK_CH6F: return gsolve_core<FamCh6F>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
-        case GK_CH6FT: return gsolve_core<FamCh6FT>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
-        case GK_CH3: return gsolve_core<FamCh3>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
-        case GK_CH3T: return gsolve_core<FamCh3T>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
-        case GK_CENT: return gsolve_core<FamCent>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
-        case GK_BOXT: return gsolve_core<FamBoxT>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s);
+        case GK_BOX: return gsolve_core<FamBox>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s, total);
+        case GK_CH6F: return gsolve_core<FamCh6F>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s, total);
+        case GK_CH6FT: return gsolve_core<FamCh6FT>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s, total);
+        case GK_CH3: return gsolve_core<FamCh3>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s, total);
+        case GK_CH3T: return gsolve_core<FamCh3T>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s, total);
+        case GK_CENT: return gsolve_core<FamCent>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s, total);
+        case GK_BOXT: return gsolve_core<FamBoxT>(p, batch, x0, u0, w0, lref, o, w, st, it, kkt, obj, s, total);
     }
     return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }
@@ -2487,6 +2587,19 @@ extern "C" int mf_gsolve_batch_dev(mf_gproblem *p, int batch, const double *x0, 
     int e = capi_ensure_device();
     if (e) return e;
     return gdispatch_solve(p, batch, x0, u0, w0, line_ref, opts, w, status, iters, kkt, obj, (hipStream_t)stream);
+}
+
+// continuous batching (device memory): `slots` concurrent solves work through `total` problems; the inputs
+// (x0, u0, w0, line_ref) and outputs have `total` rows, results identical to mf_gsolve_batch_dev's
+extern "C" int mf_gsolve_stream_dev(mf_gproblem *p, int total, int slots, const double *x0, const double *u0,
+                                    const double *w0, const double *line_ref, const mf_gopts *opts, double *w,
+                                    int *status, int *iters, double *kkt, double *obj, void *stream) {
+    if (!p || !x0 || !w || total < 1 || slots < 1) return capi_fail(MF_ERR_ARG, "bad argument");
+    int e = capi_ensure_device();
+    if (e) return e;
+    if (slots > total) slots = total;
+    return gdispatch_solve(p, slots, x0, u0, w0, line_ref, opts, w, status, iters, kkt, obj, (hipStream_t)stream,
+                           total);
 }
 
 namespace {

@@ -190,6 +190,33 @@ class GOCP:
                                                   out["w"], out["status"], out["iters"], out["kkt"], out["obj"],
                                                   stream))
 
+    def solve_stream_dev(self, x0_ptr, u0_ptr, w0_ptr, lref_ptr, total: int, slots: int, out: dict, stream: int = 0,
+                         **opts) -> None:
+        """Continuous batching (mf_gsolve_stream_dev): `slots` concurrent solves work through `total` problems
+        (inputs / outputs with `total` rows, device pointers); each problem's result equals solve_dev's."""
+        o = self.opts(**opts)
+        _lib.check(_lib.lib().mf_gsolve_stream_dev(self._h, total, slots, x0_ptr, u0_ptr, w0_ptr, lref_ptr, C.byref(o),
+                                                   out["w"], out["status"], out["iters"], out["kkt"], out["obj"],
+                                                   stream))
+
+    def solve_stream(self, x0, slots: int, u0=None, w0=None, line_ref=None, **opts) -> SolveResult:
+        """Host-array convenience over solve_stream_dev (torch device buffers)."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        x0 = np.ascontiguousarray(np.atleast_2d(x0), dtype=np.float64)
+        T = x0.shape[0]
+        t = lambda a, n: None if a is None else torch.as_tensor(np.ascontiguousarray(
+            np.broadcast_to(np.asarray(a, float), (T, n))), device=dev)
+        xd, ud, wd, ld = t(x0, self.nx), t(u0, self.nu), t(w0, self.wsize), t(line_ref, 2)
+        out = {"w": torch.empty((T, self.wsize), dtype=torch.float64, device=dev),
+               "status": torch.empty(T, dtype=torch.int32, device=dev), "iters": torch.empty(T, dtype=torch.int32, device=dev),
+               "kkt": torch.empty(T, dtype=torch.float64, device=dev), "obj": torch.empty(T, dtype=torch.float64, device=dev)}
+        p = lambda a: None if a is None else a.data_ptr()
+        self.solve_stream_dev(p(xd), p(ud), p(wd), p(ld), T, slots, {k: v.data_ptr() for k, v in out.items()},
+                              stream=torch.cuda.current_stream(dev).cuda_stream, **opts)
+        torch.cuda.synchronize(dev)
+        return SolveResult(*(out[k].cpu().numpy() for k in ("w", "status", "iters", "kkt", "obj")))
+
     def node_record(self, xu, yi, ye, lam, line_ref=None, device: int = 0) -> np.ndarray:
         """One node record from the device kernel (layout: mf_gnode_record).  ye = [state rows | mixed rows];
         line_ref: the line reference (chain) or the 6 pose targets (Centauro)."""

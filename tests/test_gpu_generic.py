@@ -412,3 +412,32 @@ def test_generic_bench_workloads_match_hyperdual_oracle():
             assert np.abs(g.q_traj(r.w[i]) - g.q_traj(W[i])).max() < 1e-6, n
         r1 = g.solve(x0=X[:1], **IPOPT_KW)
         assert np.abs(r1.w[0] - r.w[0]).max() < 1e-9
+
+
+@pytest.mark.parametrize("case", ["chain_merit", "centauro_ipopt"])
+def test_stream_solve_equals_batch_solve(case):
+    """Continuous batching (mf_gsolve_stream_dev): a few slots working through many problems -- each slot
+    handed the next problem when its own finishes (x_0, line reference and warm-start rows re-staged,
+    k_gharvest) -- give every problem exactly the batch solve's result (same arithmetic per horizon)."""
+    from mpc_fatigue_amd import pin
+    rng = np.random.default_rng(3)
+    if case == "chain_merit":
+        spec = PR.pilz6_bench(N=20)
+        T, slots = 40, 7
+        Q0 = PR.pilz6_batch_q0(T, seed=5)
+        fk = pin.generate_forward_kin(PR.read_urdf(spec["urdf"]), spec["frame"])
+        LR = fk.batch(Q0)[0][:, :2]
+        X, kw = Q0, dict(F_init=PR.BENCH_F_INIT, max_soc=4, line_ref=LR)
+    else:
+        spec = PR.centauro(N=20, T=2.0)
+        T, slots = 12, 5
+        q0 = np.asarray(spec["q0"])
+        X = np.hstack([q0[None] + rng.uniform(-0.02, 0.02, (T, 14)), np.tile(spec["T0"], (T, 1))])
+        kw = dict(IPOPT_MODE)
+    g = GOCP(spec)
+    rb = g.solve(x0=X, **kw)
+    rs = g.solve_stream(X, slots, **kw)
+    np.testing.assert_array_equal(rs.status, rb.status)
+    np.testing.assert_array_equal(rs.iters, rb.iters)
+    np.testing.assert_array_equal(rs.w, rb.w)
+    assert (rb.status == 0).mean() >= 0.5

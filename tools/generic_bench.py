@@ -53,7 +53,9 @@ IPOPT_KW = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=3000, ma
 
 
 def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0, cases=("c3", "c4"),
-                  stage_caps=None, batch_c4: int | None = None, mode: str = "ipopt") -> dict:
+                  stage_caps=None, batch_c4: int | None = None, mode: str = "ipopt", slots: int = 0) -> dict:
+    """slots > 0 (single-stage IPOPT mode): continuous batching -- `slots` concurrent solves work through the
+    `batch` starts (mf_gsolve_stream_dev), so the few long solves no longer hold the device at one-horizon latency."""
     """stage_caps: iteration caps of the C3 homotopy stages (merit mode; default: 1000 each, GOCP.solve_box's)."""
     import torch
 
@@ -101,8 +103,12 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
                 ptr = {k: v.data_ptr() for k, v in ob.items()}
                 kw2 = dict(kw, max_iter=caps[i] if max_iter is None else max_iter)
                 t = time.perf_counter()
-                g.solve_dev(x.data_ptr(), None, None if prev is None else prev.data_ptr(), None, batch, ptr,
-                            stream=stream.cuda_stream, **kw2)
+                if slots and len(gs) == 1 and slots < batch:
+                    g.solve_stream_dev(x.data_ptr(), None, None, None, batch, slots, ptr, stream=stream.cuda_stream,
+                                       **kw2)
+                else:
+                    g.solve_dev(x.data_ptr(), None, None if prev is None else prev.data_ptr(), None, batch, ptr,
+                                stream=stream.cuda_stream, **kw2)
                 torch.cuda.synchronize(dev)
                 print(f"[generic_bench] {name} {label} stage {i}: {time.perf_counter() - t:.2f}s "
                       f"converged {int((ob['status'] == 0).sum().item())}/{batch}", file=sys.stderr, flush=True)
@@ -116,6 +122,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
         its = [int(b["iters"].sum().item()) for b in bufs]
         conv = int((st == 0).sum())
         rec = {"mode": mode, "value": conv / dt, "unit": "horizons/s", "batch": batch, "converged": conv,
+               "slots": (slots if (slots and len(stages) == 1 and slots < batch) else batch),
                "converged_frac": conv / batch, "seconds": dt, "stages": len(stages),
                "mean_iters_per_stage": [i / batch for i in its], "stage_max_iter": caps,
                "N": N, "nx": nx, "nu": nu, "ni": gs[0].ni}
@@ -158,8 +165,10 @@ if __name__ == "__main__":
     ap.add_argument("--sample", type=int, default=2)
     ap.add_argument("--caps", default="", help="comma list of C3 homotopy stage iteration caps (default 1000 each)")
     ap.add_argument("--mode", default="ipopt", choices=["ipopt", "merit"])
+    ap.add_argument("--slots", type=int, default=0, help="continuous batching: concurrent solves (0: the whole batch)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
     caps = [int(c) for c in a.caps.split(",")] if a.caps else None
-    print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")), stage_caps=caps, mode=a.mode)))
+    print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")), stage_caps=caps, mode=a.mode,
+                                   slots=a.slots)))
