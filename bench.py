@@ -385,8 +385,9 @@ def main() -> int:
         from generic_bench import generic_extra
         torch.cuda.set_device(dev)
         # IPOPT mode (the reference's solve: x0 = 0, filter globalisation, bound_relax 1e-8; no homotopy)
+        # (c2: the headline's own C2 horizons solved as the reference solves them, through the generic solver)
         result["generic"] = generic_extra(batch=args.generic_batch, sample=2, cpu=not args.no_cpu_baseline,
-                                          mode="ipopt")
+                                          mode="ipopt", cases=("c3", "c4", "c2"))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import pin_np as P

@@ -441,3 +441,27 @@ def test_stream_solve_equals_batch_solve(case):
     np.testing.assert_array_equal(rs.iters, rb.iters)
     np.testing.assert_array_equal(rs.w, rb.w)
     assert (rb.status == 0).mean() >= 0.5
+
+
+def test_c2_ipopt_mode_matches_oracle():
+    """C2 (force_optimization_pilz_6DOF.py) solved as the reference solves it -- nlpsol at IPOPT's defaults
+    from x0 = 0 (L195-196 pass no x0): the generic solver's chain family in IPOPT mode, two horizons of the
+    bench batch, equals the oracle's IPOPT-mode solve (q 1e-6 rad, same status).  (The headline solver starts
+    from the held state with the l1-merit search and reaches a neighbouring optimum)"""
+    from oracle import pin_np as P
+    from oracle.urdf_np import load_urdf_file
+    N = 100
+    base = PR.pilz6_bench(N=N)
+    ref = load_urdf_file(PR.urdf_path(base["urdf"]))
+    Q0 = PR.pilz6_batch_q0(2, seed=0)
+    LR = np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in Q0])
+    kw = dict(IPOPT_MODE, max_iter=3000)
+    r = GOCP(base).solve(x0=Q0, line_ref=LR, **kw)
+    specs = [PR.pilz6_bench(N=N, q0=Q0[b], line_ref=LR[b]) for b in range(2)]
+    # the oracle with the device's KKT elimination (Riccati): on horizon 0 the last node's q_3 is weakly
+    # determined (the oracle's banded and Riccati eliminations end 0.016 rad apart, objectives 3e-7 apart)
+    W, R = G.solve_batch(specs, nthreads=2, resto_hard_dyn=True, riccati=True, **kw)
+    g = GOCP(base)
+    for b in range(2):
+        assert int(r.status[b]) == R[b].status == 0, (b, int(r.status[b]), R[b].status)
+        assert np.abs(g.q_traj(r.w[b]) - g.q_traj(W[b])).max() < 1e-6

@@ -84,6 +84,13 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
         cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(IPOPT_KW)))
     else:
         cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(u_init=PR.centauro_u_init(sp4), max_iter=500, max_soc=4)))
+    lrefs = {}
+    if "c2" in todo:  # C2 as the reference solves it (IPOPT from x0 = 0) on the C5 batch's horizons
+        from mpc_fatigue_amd import pin
+        sp2 = PR.pilz6_bench(N=100)
+        Q2 = PR.pilz6_batch_q0(batch, seed=0)
+        lrefs["c2_pilz6_n100_ipopt"] = pin.generate_forward_kin(PR.read_urdf(sp2["urdf"]), sp2["frame"]).batch(Q2)[0][:, :2]
+        cases.append(("c2_pilz6_n100_ipopt", sp2, Q2, [sp2], dict(IPOPT_KW)))
     cases = [c for c in cases if c[0][:2] in todo]
     for name, spec, X, stages, kw in cases:
         batch = X.shape[0]
@@ -91,6 +98,9 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
         gs = [GOCP(st) for st in stages]
         nx, nu, N = gs[0].nx, gs[0].nu, spec["N"]
         x = torch.as_tensor(X, dtype=torch.float64, device=dev).contiguous()
+        lr = (torch.as_tensor(np.ascontiguousarray(lrefs[name]), dtype=torch.float64, device=dev)
+              if name in lrefs else None)
+        lrp = None if lr is None else lr.data_ptr()
         bufs = [{"w": torch.empty((batch, gs[0].wsize), dtype=torch.float64, device=dev),
                  "status": torch.empty(batch, dtype=torch.int32, device=dev),
                  "iters": torch.empty(batch, dtype=torch.int32, device=dev),
@@ -104,10 +114,10 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
                 kw2 = dict(kw, max_iter=caps[i] if max_iter is None else max_iter)
                 t = time.perf_counter()
                 if slots and len(gs) == 1 and slots < batch:
-                    g.solve_stream_dev(x.data_ptr(), None, None, None, batch, slots, ptr, stream=stream.cuda_stream,
+                    g.solve_stream_dev(x.data_ptr(), None, None, lrp, batch, slots, ptr, stream=stream.cuda_stream,
                                        **kw2)
                 else:
-                    g.solve_dev(x.data_ptr(), None, None if prev is None else prev.data_ptr(), None, batch, ptr,
+                    g.solve_dev(x.data_ptr(), None, None if prev is None else prev.data_ptr(), lrp, batch, ptr,
                                 stream=stream.cuda_stream, **kw2)
                 torch.cuda.synchronize(dev)
                 print(f"[generic_bench] {name} {label} stage {i}: {time.perf_counter() - t:.2f}s "
@@ -121,12 +131,14 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
         st = bufs[-1]["status"].cpu().numpy()
         its = [int(b["iters"].sum().item()) for b in bufs]
         conv = int((st == 0).sum())
+        sv, sc = np.unique(st, return_counts=True)
         rec = {"mode": mode, "value": conv / dt, "unit": "horizons/s", "batch": batch, "converged": conv,
+               "status_counts": {int(a): int(c) for a, c in zip(sv, sc)},
                "slots": (slots if (slots and len(stages) == 1 and slots < batch) else batch),
                "converged_frac": conv / batch, "seconds": dt, "stages": len(stages),
                "mean_iters_per_stage": [i / batch for i in its], "stage_max_iter": caps,
                "N": N, "nx": nx, "nu": nu, "ni": gs[0].ni}
-        if cpu and sample > 0:
+        if cpu and sample > 0 and name not in lrefs:
             from oracle import cpu_fast as CF
             from oracle import generic as G
             fk = CF.FastNodes(spec)
