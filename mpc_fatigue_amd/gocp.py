@@ -205,8 +205,8 @@ class GOCP:
         dev = torch.device("cuda", torch.cuda.current_device())
         x0 = np.ascontiguousarray(np.atleast_2d(x0), dtype=np.float64)
         T = x0.shape[0]
-        t = lambda a, n: None if a is None else torch.as_tensor(np.ascontiguousarray(
-            np.broadcast_to(np.asarray(a, float), (T, n))), device=dev)
+        t = lambda a, n: None if a is None else torch.as_tensor(
+            np.broadcast_to(np.asarray(a, float), (T, n)).copy(), device=dev)
         xd, ud, wd, ld = t(x0, self.nx), t(u0, self.nu), t(w0, self.wsize), t(line_ref, 2)
         out = {"w": torch.empty((T, self.wsize), dtype=torch.float64, device=dev),
                "status": torch.empty(T, dtype=torch.int32, device=dev), "iters": torch.empty(T, dtype=torch.int32, device=dev),
