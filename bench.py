@@ -386,8 +386,10 @@ def main() -> int:
         torch.cuda.set_device(dev)
         # IPOPT mode (the reference's solve: x0 = 0, filter globalisation, bound_relax 1e-8; no homotopy)
         # (c2: the headline's own C2 horizons solved as the reference solves them, through the generic solver)
+        # (cap 1500: IPOPT's default 3000 only adds the last few starts' single-horizon tail, ~45 s per case, to
+        # the default run; the 3000-cap figures: profiles/r04f_bench_default.json)
         result["generic"] = generic_extra(batch=args.generic_batch, sample=2, cpu=not args.no_cpu_baseline,
-                                          mode="ipopt", cases=("c3", "c4", "c2"))
+                                          mode="ipopt", cases=("c3", "c4", "c2"), max_iter=1500)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         from oracle import pin_np as P

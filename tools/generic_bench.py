@@ -53,7 +53,8 @@ IPOPT_KW = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=3000, ma
 
 
 def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: int = 0, cases=("c3", "c4"),
-                  stage_caps=None, batch_c4: int | None = None, mode: str = "ipopt", slots: int = 0) -> dict:
+                  stage_caps=None, batch_c4: int | None = None, mode: str = "ipopt", slots: int = 0,
+                  max_iter: int = 0) -> dict:
     """slots > 0 (single-stage IPOPT mode): continuous batching -- `slots` concurrent solves work through the
     `batch` starts (mf_gsolve_stream_dev), so the few long solves no longer hold the device at one-horizon latency."""
     """stage_caps: iteration caps of the C3 homotopy stages (merit mode; default: 1000 each, GOCP.solve_box's)."""
@@ -65,6 +66,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
     dev = torch.device("cuda", torch.cuda.current_device())
     stream = torch.cuda.current_stream(dev)
     rng = np.random.default_rng(seed)
+    cap = {"max_iter": max_iter} if max_iter else {}
     out = {}
     todo = cases
     cases = []
@@ -72,7 +74,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
     sp3 = PR.box_shared_fatigue(N=100, q0=q0b)
     X3 = np.hstack([q0b[None] + rng.uniform(-0.01, 0.01, (batch, 12)), np.tile(sp3["T0"], (batch, 1))])
     if mode == "ipopt":
-        cases.append(("c3_shared_budget_n100", sp3, X3, [sp3], dict(IPOPT_KW)))
+        cases.append(("c3_shared_budget_n100", sp3, X3, [sp3], dict(IPOPT_KW, **cap)))
     else:
         cases.append(("c3_shared_budget_n100", sp3, X3, [dict(sp3, pos_toll=t) for t in PR.box_homotopy_tolerances()],
                       dict(u_init=PR.box_u_init(sp3), max_iter=1000, max_soc=4)))
@@ -81,7 +83,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
     b4 = batch_c4 or batch
     X4 = np.hstack([q0c[None] + rng.uniform(-0.02, 0.02, (b4, 14)), np.tile(sp4["T0"], (b4, 1))])
     if mode == "ipopt":
-        cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(IPOPT_KW)))
+        cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(IPOPT_KW, **cap)))
     else:
         cases.append(("c4_centauro_n50", sp4, X4, [sp4], dict(u_init=PR.centauro_u_init(sp4), max_iter=500, max_soc=4)))
     lrefs = {}
@@ -90,7 +92,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
         sp2 = PR.pilz6_bench(N=100)
         Q2 = PR.pilz6_batch_q0(batch, seed=0)
         lrefs["c2_pilz6_n100_ipopt"] = pin.generate_forward_kin(PR.read_urdf(sp2["urdf"]), sp2["frame"]).batch(Q2)[0][:, :2]
-        cases.append(("c2_pilz6_n100_ipopt", sp2, Q2, [sp2], dict(IPOPT_KW)))
+        cases.append(("c2_pilz6_n100_ipopt", sp2, Q2, [sp2], dict(IPOPT_KW, **cap)))
     cases = [c for c in cases if c[0][:2] in todo]
     for name, spec, X, stages, kw in cases:
         batch = X.shape[0]
