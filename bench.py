@@ -297,6 +297,18 @@ def main() -> int:
                     "flops_per_launch": fl,
                     "note": "executed FP64 VALU flops (PMC SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 x 64, per node evaluation "
                             "of the same workload, profiles/pmc_traffic.json) over this run's launch time"}
+    # algorithmic FP64 work: op-counted on the device templates (tools/flopcount.py, profiles/fp64_opcount.json)
+    opc_path = os.path.join(ROOT, "profiles", "fp64_opcount.json")
+    if os.path.exists(opc_path):
+        with open(opc_path) as f:
+            opc = json.load(f)
+        fla = opc["eval_phase_ops_per_node_eval"] * total_bytes / NODE_BYTES / max(1, ev_launches)
+        tfa = fla / (per_launch_ms / 1e3) / 1e12
+        algo = {"achieved": tfa, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": tfa / FP64_PEAK_TFS,
+                "flops_per_launch": fla, "ops_per_node_eval": opc["eval_phase_ops_per_node_eval"],
+                "note": "op-counted algorithmic FP64 work of the eval phase's lanes per node evaluation "
+                        "(profiles/fp64_opcount.json) over this run's launch time"}
+        fp64 = dict(algo, executed=fp64)
     total_ms = sum(v[0] for v in stats.values())
     roofline = {
         "kernel": "k_eval_node", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
