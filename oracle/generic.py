@@ -73,6 +73,8 @@ def lib():
         L.mfg_solve_batch.argtypes = [dp, dp, C.POINTER(GOCP), C.c_int, C.POINTER(GOpts), dp, C.c_int,
                                       C.POINTER(O.Result), C.c_int]
         L.mfg_node_derivs.argtypes = [dp, dp, C.POINTER(GOCP), dp, dp, dp, dp, dp, dp, dp]
+        L.mfg_ric_check_max.argtypes = [C.c_int]
+        L.mfg_ric_check_max.restype = C.c_double
         _lib = L
     return _lib
 

@@ -119,7 +119,10 @@ typedef struct {
     const double *dual_in;
     /* 1: factor the KKT by the Riccati recursion the device solver runs (csrc/gipm.hip: stage blocks
      * [[Q_uu, D_u^T], [D_u, -dc]], Sylvester inertia per stage) instead of the block-tridiagonal
-     * Bunch-Kaufman factorisation; the same Newton direction up to round-off (the CPU baseline) */
+     * Bunch-Kaufman factorisation; the same Newton direction up to round-off (the CPU baseline);
+     * 2: the same in the restoration phase too (elastic dynamics rows through the relaxed recursion of
+     * ric_relax; 1 falls back to the block-tridiagonal factorisation there); 3: test mode, both factorisations
+     * in the restoration phase compared step by step (mfg_ric_check_max) */
     int riccati;
     /* 1: IPOPT's own globalisation instead of the l1-merit search (IpFilterLSAcceptor.cpp and
      * IpBacktrackingLineSearch.cpp at their defaults): the (theta, phi) filter with the switching
@@ -338,6 +341,10 @@ typedef struct {
     int ric, nk;
     double *Pg, *Kst, *Fg, *pvg, *kvg;
     int *Kpp;
+    /* relaxed dynamics rows (restoration with elastic dynamics, or dc_all): their diagonal D_r per stage and
+     * the state-equality rows of node k+1 seen through the relaxed dynamics, J~ = J_e,k+1 (I + D_r P)^-1 */
+    double *Drg, *Jtg, *LUg;
+    int *LUp;
     /* IPOPT's restoration phase (filter mode, IpRestoIpoptNLP.cpp): the same variables plus elastic
      * p, n >= 0 on every constraint row, row r in the order [dynamics (N nx) | slack rows (N ni) |
      * equality rows (N ne)], objective rho sum(p + n) + zeta/2 |D_R (w - w_R)|^2, zeta = sqrt(mu).
@@ -849,23 +856,117 @@ static void kkt_direction(ws_t *S, double mu, const double *rdyn, const double *
  *   K_k = [[Q_uu, D_u^T], [D_u, -dc]],  Q_uu = H_uu + B^T P_{k+1} B,
  * and carries the value function P_k = Q_xx + R^T K_k^{-1}... (R = [Q_ux; D_x]).  The KKT matrix has the
  * inertia (n_primal, n_dual, 0) iff every K_k has inertia (nu, rows) (Sylvester). */
+/* Relaxed dynamics rows (the restoration phase's elastic p, n on the dynamics rows, or dc_all): the row
+ * reads dx_{k+1} = A dx_k + B du_k + r - D_r dlam_k with D_r >= 0 diagonal.  With dlam_k = P dx_{k+1} + p +
+ * J_n^T dy_s (P, p the value function of node k+1, J_n its state-equality rows) the elimination of dx_{k+1}
+ * leaves the hard recursion with, for L = I + P D_r (LU with partial pivoting, kept per stage),
+ *   P~ = L^-1 P = P (I + D_r P)^-1,   J~^T = L^-1 J_n^T,   p~ = L^-1 p,
+ *   the state-equality block -dc - J~ D_r J_n^T,   tv = p~ + P~ r,   z_s = req + J~ r - J_n D_r p~
+ * in place of P, J_n, -dc, p + P r, req + J_n r.  (Solves, not the Woodbury difference P - P S G^-1 S P,
+ * which cancels to a few digits once P >> 1 / D_r.)  G = I + S P S, S = D_r^(1/2), must have the inertia
+ * (nx, 0, 0) for the eliminated (x_{k+1}, lam_k) pair to contribute (nx, nx, 0).  The forward pass recovers
+ * dx_{k+1} = z - D_r dlam_k. */
+static int lu_factor(double *M, int n, int *pv) {
+    for (int c = 0; c < n; c++) {
+        int pr = c;
+        for (int r = c + 1; r < n; r++)
+            if (fabs(M[r * n + c]) > fabs(M[pr * n + c])) pr = r;
+        pv[c] = pr;
+        if (M[pr * n + c] == 0.0) return 1;
+        if (pr != c)
+            for (int j = 0; j < n; j++) { const double t = M[c * n + j]; M[c * n + j] = M[pr * n + j]; M[pr * n + j] = t; }
+        for (int r = c + 1; r < n; r++) {
+            const double f = M[r * n + c] / M[c * n + c];
+            M[r * n + c] = f;
+            for (int j = c + 1; j < n; j++) M[r * n + j] -= f * M[c * n + j];
+        }
+    }
+    return 0;
+}
+static void lu_solve(const double *M, int n, const int *pv, double *b) {
+    for (int c = 0; c < n; c++)  /* the row interchanges first: they also moved the stored multipliers */
+        if (pv[c] != c) { const double t = b[c]; b[c] = b[pv[c]]; b[pv[c]] = t; }
+    for (int c = 0; c < n; c++)
+        for (int r = c + 1; r < n; r++) b[r] -= M[r * n + c] * b[c];
+    for (int c = n - 1; c >= 0; c--) {
+        for (int j = c + 1; j < n; j++) b[c] -= M[c * n + j] * b[j];
+        b[c] /= M[c * n + c];
+    }
+}
+static int ric_relax(ws_t *S, int k, const double *Pn, double dc, double *Pt, int en) {
+    const int nx = S->nx, nes = S->nes, nv = S->nv;
+    double *Dr = S->Drg + (size_t)k * nx, *Jt = S->Jtg + (size_t)k * S->ne * nx, *L = S->LUg + (size_t)k * nx * nx;
+    int *pv = S->LUp + (size_t)k * nx;
+    const double *Jn = S->Je + (size_t)(k + 1) * S->ne * nv;
+    int any = 0;
+    for (int j = 0; j < nx; j++) {
+        Dr[j] = (S->O->dc_all ? dc : 0.0) + RDIAG(S, k * nx + j);
+        any |= Dr[j] > 0.0;
+    }
+    memcpy(Pt, Pn, sizeof(double) * nx * nx);
+    if (en)
+        for (int e = 0; e < nes; e++)
+            for (int j = 0; j < nx; j++) Jt[e * nx + j] = Jn[e * nv + j];
+    if (!any) { pv[0] = -1; return 0; }  /* hard rows: L = I */
+    double G[GX * GX], sq[GX];
+    int gp[2 * GX], np, nn, nz;
+    for (int j = 0; j < nx; j++) sq[j] = sqrt(Dr[j]);
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < nx; j++) G[i * nx + j] = (i == j ? 1.0 : 0.0) + sq[i] * Pn[i * nx + j] * sq[j];
+    bk_factor(G, nx, gp, gp + nx, &np, &nn, &nz);
+    if (nz || nn) return 1;
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < nx; j++) L[i * nx + j] = (i == j ? 1.0 : 0.0) + Pn[i * nx + j] * Dr[j];
+    if (lu_factor(L, nx, pv)) return 1;
+    for (int j = 0; j < nx; j++) { /* P~ column j */
+        double col[GX];
+        for (int i = 0; i < nx; i++) col[i] = Pn[i * nx + j];
+        lu_solve(L, nx, pv, col);
+        for (int i = 0; i < nx; i++) Pt[i * nx + j] = col[i];
+    }
+    for (int i = 0; i < nx; i++)
+        for (int j = 0; j < i; j++) Pt[i * nx + j] = Pt[j * nx + i] = 0.5 * (Pt[i * nx + j] + Pt[j * nx + i]);
+    if (en)
+        for (int e = 0; e < nes; e++) lu_solve(L, nx, pv, Jt + e * nx);
+    return 0;
+}
+/* p~ = L^-1 p of stage k (identity on hard rows) */
+static void ric_ptilde(const ws_t *S, int k, const double *p, double *pt) {
+    const int nx = S->nx;
+    memcpy(pt, p, sizeof(double) * nx);
+    if (S->LUp[(size_t)k * nx] >= 0) lu_solve(S->LUg + (size_t)k * nx * nx, nx, S->LUp + (size_t)k * nx, pt);
+}
+
+/* state-equality block of stage k under relaxed dynamics: E = J~ D_r J_n^T */
+static double ric_eblock(const ws_t *S, int k, int e1, int e2) {
+    const int nx = S->nx, nv = S->nv;
+    const double *Dr = S->Drg + (size_t)k * nx, *Jt = S->Jtg + (size_t)k * S->ne * nx;
+    const double *Jn = S->Je + (size_t)(k + 1) * S->ne * nv;
+    double acc = 0.0;
+    for (int l = 0; l < nx; l++) acc += Jt[e1 * nx + l] * Dr[l] * Jn[e2 * nv + l];
+    return acc;
+}
+
 static int kkt_factor_ric(ws_t *S, double dw, double dc, double d1) {
     const mfg_ocp *P = S->P;
     const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne, nes = S->nes, nk = S->nk;
     S->dw = dw; S->dc = dc; S->d1 = d1;
     double Pn[GX * GX], H[GV * GV], T1[GX * GU], T2[GX * GX], K[BKMAX * BKMAX], Rh[BKMAX * GX], Qxx[GX * GX];
-    double Dd[GI];
+    double Dd[GI], Pt[GX * GX];
+    const int oE = N * nx + N * ni;
     for (int i = 0; i < nx; i++)
         for (int j = 0; j < nx; j++) Pn[i * nx + j] = (i == j) ? S->Sx[N * nx + i] + dw : 0.0;
     for (int k = N - 1; k >= 0; k--) {
         const double *A = S->Af + (size_t)k * nx * nx, *B = S->Bf + (size_t)k * nx * nu;
         const double *W = S->W + (size_t)k * nv * nv, *Ji = S->Ji + (size_t)k * ni * nv;
-        const double *Je = S->Je + (size_t)k * ne * nv, *Jn = S->Je + (size_t)(k + 1) * ne * nv;
+        const double *Je = S->Je + (size_t)k * ne * nv, *Jn = S->Jtg + (size_t)k * ne * nx;
         const int en = (k + 1 < N) && EQ_ON(S, k + 1, 0) && nes > 0;
+        if (ric_relax(S, k, Pn, dc, Pt, en)) return 1;
+        memcpy(Pn, Pt, sizeof(double) * nx * nx);
         memcpy(S->Pg + (size_t)k * nx * nx, Pn, sizeof(double) * nx * nx);
         for (int q = 0; q < ni; q++) {
             const double sg = S->Ss[k * ni + q] + dw;
-            Dd[q] = CACT(S, k, q) ? sg / (1.0 + dc * sg) : 0.0;
+            Dd[q] = CACT(S, k, q) ? sg / (1.0 + (dc + RDIAG(S, N * nx + k * ni + q)) * sg) : 0.0;
         }
         for (int a = 0; a < nv; a++)
             for (int c = 0; c < nv; c++) {
@@ -908,14 +1009,19 @@ static int kkt_factor_ric(ws_t *S, double dw, double dc, double d1) {
                         for (int l = 0; l < nx; l++) v += B[l * nu + a] * T1[l * nu + c];
                     }
                 } else if (a >= nu && c >= nu) {
-                    const int ee = a - nu;
-                    v = (a == c) ? ((ee >= nes || en) ? -dc : -1.0) : 0.0;
+                    const int ee = a - nu, e2 = c - nu;
+                    if (ee >= nes) /* mixed row of stage k */
+                        v = (a == c) ? -dc - RDIAG(S, oE + k * ne + ee) : 0.0;
+                    else if (en && e2 < nes) /* state row of node k+1 */
+                        v = ((a == c) ? -dc - RDIAG(S, oE + (k + 1) * ne + ee) : 0.0) - ric_eblock(S, k, ee, e2);
+                    else
+                        v = (a == c) ? (en ? -dc : -1.0) : 0.0;
                 } else {
                     const int ee = (a >= nu ? a : c) - nu, uu = a >= nu ? c : a;
                     if (S->ufix[k * nu + uu]) v = 0.0;
                     else if (ee >= nes) v = Je[ee * nv + nx + uu];  /* mixed row of stage k */
                     else if (en)
-                        for (int l = 0; l < nx; l++) v += Jn[ee * nv + l] * B[l * nu + uu];
+                        for (int l = 0; l < nx; l++) v += Jn[ee * nx + l] * B[l * nu + uu];
                 }
                 K[a * nk + c] = v;
             }
@@ -931,7 +1037,7 @@ static int kkt_factor_ric(ws_t *S, double dw, double dc, double d1) {
                     } else if (a - nu >= nes) {
                         v = Je[(a - nu) * nv + j];
                     } else if (en) {
-                        for (int l = 0; l < nx; l++) v += Jn[(a - nu) * nv + l] * A[l * nx + j];
+                        for (int l = 0; l < nx; l++) v += Jn[(a - nu) * nx + l] * A[l * nx + j];
                     }
                 }
                 Rh[a * nx + j] = v;
@@ -974,14 +1080,19 @@ static int kkt_factor_ric(ws_t *S, double dw, double dc, double d1) {
 static void kkt_direction_ric(ws_t *S, double mu, const double *rdyn, const double *rin, const double *req) {
     const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne, nes = S->nes, nk = S->nk;
     const double dw = S->dw, dc = S->dc;
-    double pvs[GX], vx[GV], tv[GX], zv[BKMAX], dxs[GX], dxn[GX], duv[BKMAX];
+    const int oE = N * nx + N * ni;
+    double pvs[GX], vx[GV], tv[GX], zv[BKMAX], dxs[GX], dxn[GX], duv[BKMAX], rh[GX];
     for (int j = 0; j < nx; j++) pvs[j] = S->gx[N * nx + j] - S->lam[(N - 1) * nx + j];
     for (int k = N - 1; k >= 0; k--) {
         const double *A = S->Af + (size_t)k * nx * nx, *B = S->Bf + (size_t)k * nx * nu;
         const double *Ji = S->Ji + (size_t)k * ni * nv, *Je = S->Je + (size_t)k * ne * nv;
-        const double *Jn = S->Je + (size_t)(k + 1) * ne * nv, *Pk = S->Pg + (size_t)k * nx * nx;
+        const double *Jn = S->Jtg + (size_t)k * ne * nx, *Pk = S->Pg + (size_t)k * nx * nx;
+        const double *Dr = S->Drg + (size_t)k * nx;
         const int en = (k + 1 < N) && EQ_ON(S, k + 1, 0) && nes > 0;
         memcpy(S->pvg + (size_t)k * nx, pvs, sizeof(double) * nx);
+        double pt[GX];
+        ric_ptilde(S, k, pvs, pt);
+        for (int j = 0; j < nx; j++) rh[j] = rdyn[k * nx + j] + RCORR(S, k * nx + j);
         for (int a = 0; a < nv; a++) {
             double g = 0.0;
             if (vfree(S, k, a)) {
@@ -990,8 +1101,8 @@ static void kkt_direction_ric(ws_t *S, double mu, const double *rdyn, const doub
                     const int i = k * ni + q;
                     double w = S->yi[i];
                     if (CACT(S, k, q)) {
-                        const double sg = S->Ss[i] + dw, D = sg / (1.0 + dc * sg);
-                        w += D * (rin[i] + (S->gs[i] - S->yi[i]) / sg);
+                        const double sg = S->Ss[i] + dw, D = sg / (1.0 + (dc + RDIAG(S, N * nx + i)) * sg);
+                        w += D * (rin[i] + RCORR(S, N * nx + i) + (S->gs[i] - S->yi[i]) / sg);
                     }
                     g += Ji[q * nv + a] * w;
                 }
@@ -1008,8 +1119,8 @@ static void kkt_direction_ric(ws_t *S, double mu, const double *rdyn, const doub
             vx[a] = g;
         }
         for (int j = 0; j < nx; j++) {
-            double acc = pvs[j];
-            for (int l = 0; l < nx; l++) acc += Pk[j * nx + l] * rdyn[k * nx + l];
+            double acc = pt[j];
+            for (int l = 0; l < nx; l++) acc += Pk[j * nx + l] * rh[l];
             tv[j] = acc;
         }
         for (int a = 0; a < nk; a++) {
@@ -1020,11 +1131,12 @@ static void kkt_direction_ric(ws_t *S, double mu, const double *rdyn, const doub
                     for (int l = 0; l < nx; l++) z += B[l * nu + a] * tv[l];
                 }
             } else if (a - nu >= nes) {
-                z = req[k * ne + a - nu];
+                z = req[k * ne + a - nu] + RCORR(S, oE + k * ne + a - nu);
             } else if (en) {
                 const int ee = a - nu;
-                z = req[(k + 1) * ne + ee];
-                for (int l = 0; l < nx; l++) z += Jn[ee * nv + l] * rdyn[k * nx + l];
+                z = req[(k + 1) * ne + ee] + RCORR(S, oE + (k + 1) * ne + ee);
+                for (int l = 0; l < nx; l++)
+                    z += Jn[ee * nx + l] * rh[l] - S->Je[(size_t)(k + 1) * ne * nv + ee * nv + l] * Dr[l] * pt[l];
             }
             zv[a] = z;
         }
@@ -1047,8 +1159,9 @@ static void kkt_direction_ric(ws_t *S, double mu, const double *rdyn, const doub
     for (int e = 0; e < ne; e++) S->dye[e] = 0.0;
     for (int k = 0; k < N; k++) {
         const double *A = S->Af + (size_t)k * nx * nx, *B = S->Bf + (size_t)k * nx * nu;
-        const double *Jn = S->Je + (size_t)(k + 1) * ne * nv, *Pk = S->Pg + (size_t)k * nx * nx;
+        const double *Jn = S->Jtg + (size_t)k * ne * nx, *Pk = S->Pg + (size_t)k * nx * nx;
         const double *Fk = S->Fg + (size_t)k * nk * nx, *kv = S->kvg + (size_t)k * nk;
+        const double *Dr = S->Drg + (size_t)k * nx, *pk = S->pvg + (size_t)k * nx;
         const int en = (k + 1 < N) && EQ_ON(S, k + 1, 0) && nes > 0;
         for (int a = 0; a < nk; a++) {
             double acc = kv[a];
@@ -1057,18 +1170,24 @@ static void kkt_direction_ric(ws_t *S, double mu, const double *rdyn, const doub
             duv[a] = acc;
             if (a < nu) S->du[k * nu + a] = acc;
         }
+        /* z = A dx + B du + r; dlam = P~ z + p~ + J~^T dy_s; dx_{k+1} = z - D_r dlam */
+        double pt[GX];
+        ric_ptilde(S, k, pk, pt);
         for (int j = 0; j < nx; j++) {
-            double acc = rdyn[k * nx + j];
+            double acc = rdyn[k * nx + j] + RCORR(S, k * nx + j);
             for (int l = 0; l < nx; l++) acc += A[j * nx + l] * dxs[l];
             for (int c = 0; c < nu; c++) acc += B[j * nu + c] * duv[c];
             dxn[j] = acc;
         }
         for (int j = 0; j < nx; j++) {
-            double acc = S->pvg[(size_t)k * nx + j];
+            double acc = pt[j];
             for (int l = 0; l < nx; l++) acc += Pk[j * nx + l] * dxn[l];
             if (en)
-                for (int ee = 0; ee < nes; ee++) acc += Jn[ee * nv + j] * duv[nu + ee];
+                for (int ee = 0; ee < nes; ee++) acc += Jn[ee * nx + j] * duv[nu + ee];
             S->dlam[k * nx + j] = acc;
+        }
+        for (int j = 0; j < nx; j++) {
+            dxn[j] -= Dr[j] * S->dlam[k * nx + j];
             S->dx[(k + 1) * nx + j] = dxn[j];
         }
         if (k + 1 < N)
@@ -1500,7 +1619,7 @@ static void barrier_f(ws_t *S, double mu) {
  * one, or last far below) or x8 up to 1e40; a singular matrix first gets delta_c = 1e-8 mu^(1/4) */
 static int factor_f(ws_t *S, double mu, double *ic_last, int *n_ic, double *ts) {
     double dw = 0.0, dc = (S->P->dc_always || S->O->dc_all) ? 1e-8 * pow(mu, 0.25) : 0.0;
-    const int ric = S->ric && !S->resto;
+    const int ric = S->ric;  /* off in the restoration phase unless riccati >= 2 */
     for (int tries = 0; tries < 200; tries++) {
         const double t0 = wall_s();
         const int fr = ric ? kkt_factor_ric(S, dw, dc, 0.0) : kkt_factor(S, dw, dc, 0.0);
@@ -1518,8 +1637,129 @@ static int factor_f(ws_t *S, double mu, double *ic_last, int *n_ic, double *ts) 
     return 0;
 }
 
+/* riccati = 3 (test mode): in the restoration phase factor and solve both ways, keep the Riccati
+ * direction, and record the largest difference of the primal-dual steps relative to their size */
+static double g_ric_check = 0.0;
+/* largest residual of the current step (dx, du, dlam, dye) in the unfactored KKT system (the rows kkt_factor
+ * assembles: stationarity of the free x_k, u_k; dynamics; equality rows) */
+static double kkt_resid(const ws_t *S, const double *rdyn, const double *rin, const double *req) {
+    const int N = S->N, nx = S->nx, nu = S->nu, nv = S->nv, ni = S->ni, ne = S->ne;
+    const double dw = S->dw, dc = S->dc, d1 = S->d1;
+    double res = 0.0;
+    for (int k = 0; k <= N; k++) {
+        if (k == N) {
+            for (int j = 0; j < nx; j++)
+                res = fmax(res, fabs((S->Sx[N * nx + j] + dw) * S->dx[N * nx + j] - S->dlam[(N - 1) * nx + j] +
+                                     S->gx[N * nx + j] - S->lam[(N - 1) * nx + j]));
+            break;
+        }
+        const double *A = S->Af + (size_t)k * nx * nx, *B = S->Bf + (size_t)k * nx * nu;
+        const double *W = S->W + (size_t)k * nv * nv, *Ji = S->Ji + (size_t)k * ni * nv;
+        const double *Je = S->Je + (size_t)k * ne * nv;
+        double dv[GV], Dd[GI], rdd[GI];
+        for (int a = 0; a < nv; a++) dv[a] = !vfree(S, k, a) ? 0.0 : (a < nx ? S->dx[k * nx + a] : S->du[k * nu + a - nx]);
+        for (int q = 0; q < ni; q++) {
+            const int i = k * ni + q;
+            if (CACT(S, k, q)) {
+                const double sg = S->Ss[i] + dw;
+                Dd[q] = sg / (1.0 + (dc + RDIAG(S, N * nx + i)) * sg);
+                rdd[q] = rin[i] + RCORR(S, N * nx + i) + (S->gs[i] - S->yi[i]) / sg;
+            } else { Dd[q] = 0; rdd[q] = 0; }
+        }
+        for (int a = 0; a < nv; a++) {
+            if (!vfree(S, k, a)) continue;
+            double g = S->gl[k * nv + a], v = 0.0;
+            for (int q = 0; q < ni; q++) g += Ji[q * nv + a] * (S->yi[k * ni + q] + Dd[q] * rdd[q]);
+            for (int c = 0; c < nv; c++) {
+                double h = W[a * nv + c];
+                for (int q = 0; q < ni; q++) h += Ji[q * nv + a] * Dd[q] * Ji[q * nv + c];
+                v += h * dv[c];
+            }
+            if (a < nx) {
+                v += (S->Sx[k * nx + a] + dw) * dv[a];
+                g += S->gx[k * nx + a] - (k > 0 ? S->lam[(k - 1) * nx + a] : 0.0);
+                if (k > 0) v -= S->dlam[(k - 1) * nx + a];
+                for (int jj = 0; jj < nx; jj++) {
+                    g += A[jj * nx + a] * S->lam[k * nx + jj];
+                    v += A[jj * nx + a] * S->dlam[k * nx + jj];
+                }
+            } else {
+                v += (S->Su[k * nu + a - nx] + dw) * dv[a];
+                if (a - nx >= S->P->tier1_from && a - nx < S->P->tier1_to) v += d1 * dv[a];
+                g += S->gu[k * nu + a - nx];
+                for (int jj = 0; jj < nx; jj++) {
+                    g += B[jj * nu + a - nx] * S->lam[k * nx + jj];
+                    v += B[jj * nu + a - nx] * S->dlam[k * nx + jj];
+                }
+            }
+            for (int e = 0; e < ne; e++)
+                if (EQ_ON(S, k, e)) {
+                    g += Je[e * nv + a] * S->ye[k * ne + e];
+                    v += Je[e * nv + a] * S->dye[k * ne + e];
+                }
+            res = fmax(res, fabs(v + g));
+        }
+        for (int e = 0; e < ne; e++) {
+            if (!EQ_ON(S, k, e)) continue;
+            const int rr = N * nx + N * ni + k * ne + e;
+            double v = -(dc + RDIAG(S, rr)) * S->dye[k * ne + e] + req[k * ne + e] + RCORR(S, rr);
+            for (int a = 0; a < nv; a++) v += Je[e * nv + a] * dv[a];
+            res = fmax(res, fabs(v));
+        }
+        for (int j = 0; j < nx; j++) {
+            const int rr = k * nx + j;
+            const double Dr = (S->O->dc_all ? dc : 0.0) + RDIAG(S, rr);
+            double v = -S->dx[(k + 1) * nx + j] - Dr * S->dlam[rr] + rdyn[rr] + RCORR(S, rr);
+            for (int l = 0; l < nx; l++) v += A[j * nx + l] * dv[l];
+            for (int c = 0; c < nu; c++) v += B[j * nu + c] * dv[nx + c];
+            res = fmax(res, fabs(v));
+        }
+    }
+    return res;
+}
+double mfg_ric_check_max(int reset) {
+    const double v = g_ric_check;
+    if (reset) g_ric_check = 0.0;
+    return v;
+}
 static void direction_f(ws_t *S, double mu, const double *rdyn, const double *rin, const double *req) {
-    if (S->ric && !S->resto) kkt_direction_ric(S, mu, rdyn, rin, req);
+    if (S->ric && S->resto && S->O->riccati == 3) {
+        const int N = S->N, nx = S->nx, nu = S->nu, ne = S->ne;
+        const size_t nX = (size_t)(N + 1) * nx, nU = (size_t)N * nu, nL = (size_t)N * nx, nE = (size_t)N * ne;
+        double *sv = dal(nX + nU + nL + nE);
+        const double dw = S->dw, dc = S->dc, d1 = S->d1;
+        if (kkt_factor(S, dw, dc, d1) == 0) {
+            kkt_direction(S, mu, rdyn, rin, req);
+            const double res_b = getenv("MFG_RIC_DEBUG") ? kkt_resid(S, rdyn, rin, req) : 0.0;
+            memcpy(sv, S->dx, nX * sizeof(double));
+            memcpy(sv + nX, S->du, nU * sizeof(double));
+            memcpy(sv + nX + nU, S->dlam, nL * sizeof(double));
+            memcpy(sv + nX + nU + nL, S->dye, nE * sizeof(double));
+            kkt_factor_ric(S, dw, dc, d1);
+            kkt_direction_ric(S, mu, rdyn, rin, req);
+            const double *cur[4] = {S->dx, S->du, S->dlam, S->dye};
+            const size_t len[4] = {nX, nU, nL, nE};
+            double dmax = 0.0, vmax = 1e-300;
+            for (int t = 0, o = 0; t < 4; o += (int)len[t], t++)
+                for (size_t i = 0; i < len[t]; i++) {
+                    dmax = fmax(dmax, fabs(cur[t][i] - sv[o + i]));
+                    vmax = fmax(vmax, fabs(sv[o + i]));
+                }
+            g_ric_check = fmax(g_ric_check, dmax / vmax);
+            if (getenv("MFG_RIC_DEBUG") && dmax / vmax > 1e-6) {
+                double drmax = 0, drmin = 1e300;
+                for (size_t i = 0; i < nL; i++) { drmax = fmax(drmax, S->Drg[i]); drmin = fmin(drmin, S->Drg[i]); }
+                fprintf(stderr, "ric check rel %.2e vmax %.2e Dr [%.2e, %.2e] dw %.2e dc %.2e  KKT residual banded %.2e riccati %.2e\n",
+                        dmax / vmax, vmax, drmin, drmax, dw, dc, res_b, kkt_resid(S, rdyn, rin, req));
+            }
+        } else {
+            kkt_factor_ric(S, dw, dc, d1);
+            kkt_direction_ric(S, mu, rdyn, rin, req);
+        }
+        free(sv);
+        return;
+    }
+    if (S->ric) kkt_direction_ric(S, mu, rdyn, rin, req);
     else kkt_direction(S, mu, rdyn, rin, req);
 }
 
@@ -1748,7 +1988,8 @@ static int resto_phase(ws_t *S, fst_t *Fm, double thc, int *it, fcount_t *C) {
                          (size_t)N * ni};
     for (int a = 0; a < 6; a++)
         for (size_t i = 0; i < zl[a]; i++) zs[a][i] = fmin(zs[a][i], rho);
-    S->resto = 1; S->objw = 0.0; S->rho_r = rho; S->zeta = sqrt(mu_r); S->ric = 0;
+    S->resto = 1; S->objw = 0.0; S->rho_r = rho; S->zeta = sqrt(mu_r);
+    if (S->O->riccati < 2) S->ric = 0;
     eval_all(S, C->ts);
     ls_mults(S);
     fst_t Fr;
@@ -1982,6 +2223,8 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
         S->Pg = dal((size_t)N * nx * nx); S->Kst = dal((size_t)N * S->nk * S->nk); S->Fg = dal((size_t)N * S->nk * nx);
         S->pvg = dal((size_t)N * nx); S->kvg = dal((size_t)N * S->nk);
         S->Kpp = (int *)calloc((size_t)N * 2 * S->nk, sizeof(int));
+        S->Drg = dal((size_t)N * nx); S->Jtg = dal((size_t)N * ne * nx); S->LUg = dal((size_t)N * nx * nx);
+        S->LUp = (int *)calloc((size_t)N * nx, sizeof(int));
     }
     S->perm = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
     S->piv = (int *)calloc((size_t)(N + 1) * mb, sizeof(int));
@@ -2388,7 +2631,10 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
                      &S->trdyn, &S->trin, &S->treq, &S->sdyn, &S->sin_, &S->seq, &S->bk};
     for (size_t i = 0; i < sizeof pp / sizeof pp[0]; i++) free(*pp[i]);
     free(S->ufix); free(S->perm); free(S->piv);
-    if (S->ric) { free(S->Pg); free(S->Kst); free(S->Fg); free(S->pvg); free(S->kvg); free(S->Kpp); }
+    if (S->ric) {
+        free(S->Pg); free(S->Kst); free(S->Fg); free(S->pvg); free(S->kvg); free(S->Kpp); free(S->Drg); free(S->Jtg);
+        free(S->LUg); free(S->LUp);
+    }
     if (O->filter) {
         double **ra[] = {&S->pr, &S->nr, &S->zp, &S->zn, &S->dpr, &S->dnr, &S->dzp, &S->dzn, &S->tpr, &S->tnr,
                          &S->Sp, &S->Sn, &S->gp, &S->gn, &S->rowr, &S->wR, &S->dR};
