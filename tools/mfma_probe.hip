@@ -1,11 +1,13 @@
 // Probe (not product code): one wavefront forms C = A B for the generic solver's stage-product shapes
-// (M x K times K x N, FP64, operands in LDS) repeatedly, (a) the register-tiled VALU way of tile_gemm
-// (bk_wave.hpp: each lane a tile of outputs, the operands of one inner index read once per tile) and
+// (M x K times K x N, FP64, operands in LDS) repeatedly, (a) the product's tile_gemm (bk_wave.hpp: each
+// lane a register tile of outputs, the operands of one inner index read once per tile) and
 // (b) with v_mfma_f64_16x16x4_f64 on zero-padded 16 x 16 output tiles and 4-deep K steps; prints cycles per
 // product (s_memtime) and the largest difference of the two results.  DESIGN.md s.9 records the outcome.
 //
 //   hipcc -O3 --offload-arch=gfx950 tools/mfma_probe.hip -o /tmp/mfma_probe && /tmp/mfma_probe
 #include <hip/hip_runtime.h>
+
+#include "../mpc_fatigue_amd/csrc/bk_wave.hpp"
 
 #include <cmath>
 #include <cstdio>
@@ -21,54 +23,59 @@ __global__ __launch_bounds__(64) void k_probe(const double *A, const double *B, 
     for (int e = lane; e < M * K; e += 64) As[e] = A[e];
     for (int e = lane; e < K * N; e += 64) Bs[e] = B[e];
     __syncthreads();
-    // (a) VALU, register tile: lane owns outputs e = lane + 64 t
-    constexpr int NE = (M * N + 63) / 64;
+    // (a) VALU: the product's tile_gemm
     long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps; r++) {
-        double acc[NE];
-#pragma unroll
-        for (int t = 0; t < NE; t++) acc[t] = 0.0;
-        for (int k = 0; k < K; k++) {
-#pragma unroll
-            for (int t = 0; t < NE; t++) {
-                const int e = lane + 64 * t;
-                if (e < M * N) acc[t] += As[(e / N) * K + k] * Bs[k * N + e % N];
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < NE; t++) {
-            const int e = lane + 64 * t;
-            if (e < M * N) Cs[e] = acc[t] + 1e-300 * r;
-        }
+        mf::tile_gemm<M, N, K>(
+            lane, [&](int, int) { return 1e-300 * r; }, [&](int l, int i) { return As[i * K + l]; },
+            [&](int l, int j) { return Bs[l * N + j]; }, [&](int i, int j, double v) { Cs[i * N + j] = v; });
         __syncthreads();
     }
     long long t1 = __builtin_amdgcn_s_memtime();
     for (int e = lane; e < M * N; e += 64) Cv[e] = Cs[e];
     __syncthreads();
     // (b) MFMA 16x16x4 f64: A operand lane l -> (row l%16, k l/16), B operand (k l/16, col l%16),
-    // result lane l -> col l%16, rows 4 (l/16) + 0..3
+    // result lane l, register q -> (row l/16 + 4 q, col l%16)
     constexpr int TM = (M + 15) / 16, TN = (N + 15) / 16, TK = (K + 3) / 4;
     const int i16 = lane % 16, k4 = lane / 16;
+    __syncthreads();
     long long t2 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps; r++) {
+        // all TM x TN accumulators live at once; per K step the fragments are loaded once and the
+        // TM x TN independent MFMAs issue back to back (no dependent chain between neighbours)
+        v4d c[TM][TN];
 #pragma unroll
         for (int tm = 0; tm < TM; tm++)
 #pragma unroll
-            for (int tn = 0; tn < TN; tn++) {
-                v4d c = {0.0, 0.0, 0.0, 0.0};
+            for (int tn = 0; tn < TN; tn++) c[tm][tn] = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int tk = 0; tk < TK; tk++) {
-                    const int ai = tm * 16 + i16, ak = tk * 4 + k4, bj = tn * 16 + i16;
-                    const double a = (ai < M && ak < K) ? As[ai * K + ak] : 0.0;
-                    const double b = (ak < K && bj < N) ? Bs[ak * N + bj] : 0.0;
-                    c = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-                }
+        for (int tk = 0; tk < TK; tk++) {
+            const int ak = tk * 4 + k4;
+            double a[TM], b[TN];
+#pragma unroll
+            for (int tm = 0; tm < TM; tm++) {
+                const int ai = tm * 16 + i16;
+                a[tm] = (ai < M && ak < K) ? As[ai * K + ak] : 0.0;
+            }
+#pragma unroll
+            for (int tn = 0; tn < TN; tn++) {
+                const int bj = tn * 16 + i16;
+                b[tn] = (ak < K && bj < N) ? Bs[ak * N + bj] : 0.0;
+            }
+#pragma unroll
+            for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+                for (int tn = 0; tn < TN; tn++) c[tm][tn] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[tm], b[tn], c[tm][tn], 0, 0, 0);
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; tm++)
+#pragma unroll
+            for (int tn = 0; tn < TN; tn++)
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
-                    const int ci = tm * 16 + 4 * k4 + q, cj = tn * 16 + i16;
-                    if (ci < M && cj < N) Cs[ci * N + cj] = c[q] + 1e-300 * r;
+                    const int ci = tm * 16 + k4 + 4 * q, cj = tn * 16 + i16;
+                    if (ci < M && cj < N) Cs[ci * N + cj] = c[tm][tn][q] + 1e-300 * r;
                 }
-            }
         __syncthreads();
     }
     long long t3 = __builtin_amdgcn_s_memtime();
