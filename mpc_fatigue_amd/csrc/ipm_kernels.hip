@@ -348,8 +348,14 @@ template <int NJ, int NF, int NV> struct QOut {
         W[(NJ + i) * NV + v] = gqd.d;
     }
 };
+// MF_EVALQ_WAVES (experiment builds only): ask the register allocator for that many waves per SIMD
+#ifdef MF_EVALQ_WAVES
+#define MF_EVALQ_ATTR __attribute__((amdgpu_waves_per_eu(MF_EVALQ_WAVES)))
+#else
+#define MF_EVALQ_ATTR
+#endif
 template <int NJ, int NF, int NL>
-__global__ __launch_bounds__(64) void k_eval_q(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
+__global__ __launch_bounds__(64) MF_EVALQ_ATTR void k_eval_q(const DevModel *__restrict__ Mg, const DevFrame *__restrict__ Fg,
                                                OcpConst C, IpmArrays A, int batch) {
     constexpr int NV = 2 * NJ + NF;
     constexpr int NFA = NF > 0 ? NF : 1;
