@@ -120,6 +120,9 @@ template <int M, int N, int K> static void run(const char *what) {
 }
 
 int main() {
+    run<12, 7, 12>("C1/C5: P B (nx x nu)");
+    run<12, 12, 12>("C1/C5: P A (nx x nx)");
+    run<7, 7, 12>("C1/C5: B^T (P B)");
     run<24, 18, 24>("C3: P B (nx x nu)");
     run<24, 24, 24>("C3: P A (nx x nx)");
     run<18, 18, 24>("C3: B^T (P B) (nu x nu)");
