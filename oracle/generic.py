@@ -226,6 +226,9 @@ def w_size(g: GOCP) -> int:
 def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, verbose=0, F_init=0.0,
          w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None, node_cb=None, node_ctx=None, val_cb=None,
          warm_start=False, dual_in=None, riccati=False, filter=False, dc_all=False, resto_hard_dyn=False):
+    """mfg_opts (oracle/mf_ocp.c).  riccati: 0 block-tridiagonal KKT, 1 the device's Riccati recursion
+    (banded in the restoration phase), 2 Riccati in the restoration phase too (relaxed dynamics rows,
+    ric_relax), 3 test mode: both in the restoration phase, step difference in mfg_ric_check_max."""
     o = GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), int(verbose), F_init, None, bound_relax, None,
               max_soc, None, node_cb, node_ctx, val_cb, int(warm_start), None, int(riccati), int(filter), int(dc_all),
               int(resto_hard_dyn))
