@@ -133,16 +133,14 @@ def main() -> int:
                          "starts 20 horizons/s, 4096 starts 52, r03af)")
     ap.add_argument("--inflight", type=int, default=4,
                     help="independent steps in flight (own workspace, stream and host thread each)")
-    ap.add_argument("--hw-queues", type=int, default=0,
-                    help="HIP hardware queues of this process (GPU_MAX_HW_QUEUES, set before the runtime starts; "
-                         "0 = keep an exported GPU_MAX_HW_QUEUES, else 8): "
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="HIP hardware queues of this process (GPU_MAX_HW_QUEUES, set before the runtime starts, "
+                         "over any exported value; 0 = keep the exported value): "
                          "with the runtime's default of 4, the steps' streams and the default stream share queues "
                          "and serialise (r03ab/r03ac: 4 in flight 11.3k horizons/s on 4 queues, 12.0k on 8)")
     args = ap.parse_args()
     if args.hw_queues > 0:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.hw_queues, 32))
-    elif "GPU_MAX_HW_QUEUES" not in os.environ:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
     import torch
     import torch.distributed as dist
@@ -345,7 +343,7 @@ def main() -> int:
                    "parallelism": f"dp{world} (independent horizons; RCCL gather of solutions)",
                    "converged_per_step": converged, "converged_frac": converged / gB,
                    "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
-                   "steps_in_flight": inflight,
+                   "steps_in_flight": inflight, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
                    "tol": opts["tol"]},
         "roofline": roofline,
         "tail": tail_rec,

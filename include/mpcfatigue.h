@@ -231,8 +231,11 @@ typedef struct {
     int verbose;
     int warm_start;        /* as mf_solver_opts.warm_start (IPOPT warm_start_init_point with w0) */
     int filter;            /* 1: IPOPT's globalisation -- filter line search, watchdog, soft restoration and the
-                              restoration phase (elastic path rows, exact dynamics); 0: the l1-merit search */
+                              restoration phase (IPOPT's: elastic p, n on every constraint row, the dynamics rows
+                              included); 0: the l1-merit search */
     double bound_relax;    /* IPOPT bound_relax_factor (1e-8 in IPOPT; 0 = exact bounds) */
+    int resto_hard_dyn;    /* 1: the restoration problem keeps x_{k+1} = f(x_k, u_k) exact (no elastic variables on
+                              the dynamics rows; the build's variant before round 5); 0: IPOPT's restoration */
 } mf_gopts;
 
 int mf_gproblem_create(const mf_model *m0, const mf_model *m1, const mf_gspec *spec, mf_gproblem **out);

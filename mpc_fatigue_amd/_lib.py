@@ -74,7 +74,8 @@ class GOpts(C.Structure):
     _fields_ = [("tol", C.c_double), ("constr_viol_tol", C.c_double), ("max_iter", C.c_int),
                 ("mu_init", C.c_double), ("init_zero", C.c_int), ("F_init", C.c_double),
                 ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("verbose", C.c_int),
-                ("warm_start", C.c_int), ("filter", C.c_int), ("bound_relax", C.c_double)]
+                ("warm_start", C.c_int), ("filter", C.c_int), ("bound_relax", C.c_double),
+                ("resto_hard_dyn", C.c_int)]
 
 
 class SolverOpts(C.Structure):

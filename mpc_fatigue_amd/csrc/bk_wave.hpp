@@ -494,6 +494,60 @@ __device__ __forceinline__ void bk_solve_cols(const double *A, const int *perm, 
     wave_lds_sync();
 }
 
+// LU factorisation with partial pivoting of an n x n matrix in LDS (n <= 64, one row per lane), the order of
+// oracle/mf_ocp.c lu_factor (LAPACK getf2): at column c the row of largest |M_rc|, r >= c (the smallest index
+// among ties), is swapped in whole, then rows r > c take the multiplier M_rc / M_cc and the update of their
+// columns > c.  pi[i] = the original row now at row i (the product of the interchanges).  Returns 1 when a pivot
+// column is exactly zero (M is then partly factored).
+template <int LD>
+__device__ __forceinline__ int lu_factor_wave(double *M, int n, int *pi) {
+    const int lane = lane_opaque();
+    if (lane < n) pi[lane] = lane;
+    __syncthreads();
+    for (int c = 0; c < n; c++) {
+        double v = (lane >= c && lane < n) ? fabs(M[lane * LD + c]) : -1.0;
+        int idx = (lane >= c && lane < n) ? lane : 64;
+        wave_argmax(v, idx);
+        const int pr = idx;
+        if (M[pr * LD + c] == 0.0) return 1;
+        if (pr != c) {
+            for (int j = lane; j < n; j += 64) {
+                const double t = M[c * LD + j];
+                M[c * LD + j] = M[pr * LD + j];
+                M[pr * LD + j] = t;
+            }
+            if (lane == 0) { const int t = pi[c]; pi[c] = pi[pr]; pi[pr] = t; }
+            __syncthreads();
+        }
+        if (lane > c && lane < n) {
+            const double f = M[lane * LD + c] / M[c * LD + c];
+            M[lane * LD + c] = f;
+            for (int j = c + 1; j < n; j++) M[lane * LD + j] -= f * M[c * LD + j];
+        }
+        __syncthreads();
+    }
+    return 0;
+}
+
+// y = (LU)^-1 b for the calling lane's right-hand side, b_i = b[pi[i] * bs] (the interchanges applied), in
+// registers: the unit-lower sweep by columns, then the upper one (oracle/mf_ocp.c lu_solve, same order)
+template <int LD, int M>
+__device__ __forceinline__ void lu_solve_lane(const double *LU, const int *pi, const double *b, int bs, double *y) {
+#pragma unroll
+    for (int i = 0; i < M; i++) y[i] = b[pi[i] * bs];
+#pragma unroll
+    for (int c = 0; c < M; c++)
+#pragma unroll
+        for (int r = c + 1; r < M; r++) y[r] -= LU[r * LD + c] * y[c];
+#pragma unroll
+    for (int c = M - 1; c >= 0; c--) {
+        double acc = y[c];
+#pragma unroll
+        for (int j = c + 1; j < M; j++) acc -= LU[c * LD + j] * y[j];
+        y[c] = acc / LU[c * LD + c];
+    }
+}
+
 // bk_factor_wave with the matrix in registers (lane i holds row i, M <= 64) for the common case
 // where Bunch-Kaufman keeps the natural order: every pivot passes the first test
 // |a_kk| >= alpha max_{i>k} |a_ik| and is non-zero.  The column of step k is broadcast with

@@ -62,6 +62,7 @@ struct GParams {
     int dc_always;                         // delta_c from the first factorisation (rank-deficient rows)
     int filter;                            // IPOPT's globalisation (filter, watchdog, restoration; gipm.hip)
     int dbg;                               // trace horizon 0 (diagnostics, gipm.hip mf_gdebug_trace)
+    int resto_hard_dyn;                    // restoration phase without elastic variables on the dynamics rows
 };
 
 template <int NX_, int NU_, int NI_, int NE_, int NM_ = 0> struct GDims {

@@ -56,7 +56,13 @@ enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INER
 //   GP_LSM         k_gkkt / k_gls compute the restoration problem's least-square multipliers
 //   GP_IDLE(_RESTO) the records are stale (a restoration ended / a soft step was undone): k_gkkt and k_gls idle,
 //                  the next iteration re-evaluates (and then sets up the restoration)
-enum { GP_NONE = 0, GP_SOFT = 1, GP_RESTO = 2, GP_LSM = 3, GP_IDLE = 4, GP_IDLE_RESTO = 5 };
+//   GP_WDSOFT      the watchdog stopped (iterate and direction restored) and the backtracking search from the
+//                  stored point failed: the records describe the abandoned point, so k_gpre / k_gkkt idle while they
+//                  are re-evaluated, and k_gls then augments the filter with the stored point and starts the soft
+//                  restoration from it (oracle/mf_ocp.c ipm_filter: eval_all after StopWatchDog)
+// Iteration counts follow the oracle's: the launch rounds that only switch state (a soft step undone, the start
+// of the restoration phase, a re-evaluation) advance no iteration.
+enum { GP_NONE = 0, GP_SOFT = 1, GP_RESTO = 2, GP_LSM = 3, GP_IDLE = 4, GP_IDLE_RESTO = 5, GP_WDSOFT = 6 };
 constexpr int GFCAP = 512;  // filter entries per filter (dominated entries are dropped as IPOPT does)
 // diagnostic trace of horizon 0 in IPOPT mode (mf_gopts.verbose >= 2; mf_gdebug_trace): per iteration one row
 // from k_gpre (E_0 pieces, the restoration exit test) and one from k_gls (line search)
@@ -73,14 +79,18 @@ struct GArrays {
     double *rdyn, *rin, *req, *trdyn, *trin, *treq, *sdyn, *sin_, *seq;
     double *tx, *tu, *ts;
     double *P, *Kinv, *Kfb, *pv, *kv;
+    // IPOPT's restoration problem with elastic dynamics rows (oracle ric_relax): per stage the LU factor of
+    // I + P_{k+1} D_r with its row permutation, and J~ = J_e,k+1 (I + D_r P_{k+1})^-1
+    double *LUg, *Jtg;
     const double *u_lo, *u_hi, *c_lo, *c_hi;  // shared, N x NU / N x NI
     double *x0, *lref;                        // per problem: NX, FAM::LREF (line reference / pose targets)
     const double *u0, *w0;                    // optional per-problem fixed u_0 values / warm start
     GState *st;
     int *active;
     // IPOPT mode: filters (2 x GFCAP x (phi, theta)), watchdog / soft-restoration copies of the iterate and of
-    // the direction, and the restoration problem's elastic variables p, n >= 0 on the slack rows and the
-    // equality rows (rows [k NIA + q | N NIA + k NET + e]), with their bound multipliers, steps, trial values,
+    // the direction, and the restoration problem's elastic variables p, n >= 0 on the slack rows, the equality rows
+    // and the dynamics rows (rows [k NIA + q | N NIA + k NET + e | N (NIA + NET) + k NX + j]; the oracle orders the
+    // same rows [dynamics | slack | equality]), with their bound multipliers, steps, trial values,
     // condensed Sigma / barrier gradients / residual corrections, and the reference point w_R, D_R^2
     double *fil, *wdit, *wddir;
     double *pr, *nr, *zp, *zn, *dpr, *dnr, *dzp, *dzn, *tpr, *tnr, *Sp, *Sn, *gp, *gn, *rowr, *wR, *dR;
@@ -104,7 +114,10 @@ template <class D> struct GSz {
     __host__ __device__ size_t e() const { return N * NE; }
     __host__ __device__ size_t l() const { return N * NX; }
     __host__ __device__ size_t rec() const { return N * D::REC; }
-    __host__ __device__ size_t nr() const { return N * (NI + NE); }  // elastic rows (restoration)
+    __host__ __device__ size_t nr() const { return N * (NI + NE + NX); }  // elastic rows (restoration)
+    __host__ __device__ size_t nrd() const { return N * (NI + NE); }      // the first elastic dynamics row
+    __host__ __device__ size_t lu() const { return N * (NX * NX + NX); }  // stage LU factors + permutations
+    __host__ __device__ size_t jt() const { return N * D::NEA * NX; }
     __host__ __device__ size_t bk() const { return 3 * x() + 3 * u() + 4 * i() + l() + e() + 4 * nr(); }
     __host__ __device__ size_t wv() const { return x() + u(); }
     __host__ __device__ size_t P() const { return N * NX * NX; }
@@ -509,6 +522,10 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     __shared__ double Ks[NK * LDK], Ys[NK], Jn[NEA * NX], Dds[NIA];  // Ys: the one-column solve's scratch
     __shared__ int perm[NK], piv[NK];
     __shared__ double vx[NV], tv[NX], zv[NK], pvs[NX], dxs[NX], dxn[NX], duv[NK];
+    // elastic dynamics rows of the restoration phase (relax_stage): D_r of the stage, J~ of node k+1, p~, the LU
+    // permutation and the pivot data of G = I + S P S
+    __shared__ double Drs[NX], Jts[NEA * NX], ptv[NX];
+    __shared__ int pix[NX], permx[NX], pivx[NX];
     // stage k's record parts staged into LDS by coalesced lane-strided loads (stage_in): the inner
     // loops of the stage then read LDS, not global memory; fixed-control / active-row flags alike
     constexpr int NIA2 = NI > 0 ? NI : 1, NMA = NM > 0 ? NM : 1;
@@ -573,7 +590,9 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     const bool flt = PH == 2 ? FLT : P.filter != 0;
     const bool rsm = flt && st.mode == 1;  // the restoration problem is being solved
     constexpr double RHO_R = 1000.0, KAPPA_D = 1e-5;
-    const size_t NRo = (size_t)N * NIA;   // elastic rows: slack rows [k NIA + q], then equality rows [NRo + k NET + e]
+    const size_t NRo = (size_t)N * NIA;   // elastic rows: slack rows [k NIA + q], then equality rows [NRo + k NET + e],
+    const size_t NRD = Z.nrd();            // then dynamics rows [NRD + k NX + j] (IPOPT's restoration; not resto_hard_dyn)
+    const bool rlx = rsm && !P.resto_hard_dyn;  // the dynamics rows carry elastic variables now
     double *prr = A.pr + b * Z.nr(), *nrr = A.nr + b * Z.nr(), *zpr = A.zp + b * Z.nr(), *znr = A.zn + b * Z.nr();
     double *dpr = A.dpr + b * Z.nr(), *dnr = A.dnr + b * Z.nr(), *dzp = A.dzp + b * Z.nr(), *dzn = A.dzn + b * Z.nr();
     double *tpr = A.tpr + b * Z.nr(), *tnr = A.tnr + b * Z.nr(), *Spr = A.Sp + b * Z.nr(), *Snr = A.Sn + b * Z.nr();
@@ -581,10 +600,23 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     double *wR = A.wR + b * Z.wv(), *dR = A.dR + b * Z.wv();
     auto el_on = [&](int r) __attribute__((always_inline)) -> bool {  // elastic row r active
         if ((size_t)r < NRo) return (r % NIA) < NI && cact(r / NIA, r % NIA);
+        if ((size_t)r >= NRD) return !P.resto_hard_dyn;
         const int e = r - (int)NRo, k = e / NET, ee = e % NET;
         return ee < NEA ? (ee < NE && eqon(k)) : true;
     };
-    auto el_y = [&](int r) __attribute__((always_inline)) -> double { return (size_t)r < NRo ? yi[r] : ye[r - NRo]; };
+    auto el_y = [&](int r) __attribute__((always_inline)) -> double {
+        return (size_t)r < NRo ? yi[r] : ((size_t)r < NRD ? ye[r - NRo] : lam[r - NRD]);
+    };
+    // the constraint value of elastic row r at the current point (records current)
+    auto el_c = [&](int r) __attribute__((always_inline)) -> double {
+        if ((size_t)r < NRo) return R(r / NIA)[D::O_CI + r % NIA] - s[r];
+        if ((size_t)r >= NRD) {
+            const int e = r - (int)NRD, k = e / NX, j = e % NX;
+            return R(k)[D::O_F + j] - x[(k + 1) * NX + j];
+        }
+        const int e = r - (int)NRo, k = e / NET, ee = e % NET;
+        return ee < NEA ? R(k)[D::O_CE + ee] : R(k)[D::O_CM + ee - NEA];
+    };
     const int NRI = (int)Z.nr();
 
     // ---------------- optimality measures at the current point (records current): IPOPT's E_0 pieces and, for
@@ -657,7 +689,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         }
         for (int e = lane; e < N * NX; e += 64) {  // dynamics
             const int k = e / NX, j = e % NX;
-            const double rp = R(k)[D::O_F + j] - x[(k + 1) * NX + j];
+            const double rp = R(k)[D::O_F + j] - x[(k + 1) * NX + j] + (rlx ? nrr[NRD + e] - prr[NRD + e] : 0.0);
             pinf = fmax(pinf, fabs(rp));
             s1 += fabs(rp);
             n1++;
@@ -765,30 +797,18 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     };
 
     if constexpr (PH == 0) {
+    if (flt && st.pend == GP_WDSOFT) return;  // records of the restored point being evaluated (k_gls continues)
     if (flt && st.pend == GP_RESTO) {
         // ---------------- MinC_1NrmRestorationPhase / RestoIterateInitializer at the current point
         double cm = 0.0;
         for (int e = lane; e < N * NX; e += 64) cm = fmax(cm, fabs(R(e / NX)[D::O_F + e % NX] - x[(e / NX + 1) * NX + e % NX]));
-        for (int r = lane; r < NRI; r += 64) {
-            if (!el_on(r)) continue;
-            double c;
-            if ((size_t)r < NRo) c = R(r / NIA)[D::O_CI + r % NIA] - s[r];
-            else {
-                const int e = r - (int)NRo, k = e / NET, ee = e % NET;
-                c = ee < NEA ? R(k)[D::O_CE + ee] : R(k)[D::O_CM + ee - NEA];
-            }
-            cm = fmax(cm, fabs(c));
-        }
+        for (int r = lane; r < (int)NRD; r += 64)
+            if (el_on(r)) cm = fmax(cm, fabs(el_c(r)));
         cm = wave_max(cm);
         const double mu_r = fmax(mu, cm);
         for (int r = lane; r < NRI; r += 64) {
             if (!el_on(r)) { prr[r] = nrr[r] = 1.0; zpr[r] = znr[r] = 0.0; continue; }
-            double c;
-            if ((size_t)r < NRo) c = R(r / NIA)[D::O_CI + r % NIA] - s[r];
-            else {
-                const int e = r - (int)NRo, k = e / NET, ee = e % NET;
-                c = ee < NEA ? R(k)[D::O_CE + ee] : R(k)[D::O_CM + ee - NEA];
-            }
+            const double c = el_c(r);
             const double a = (mu_r - RHO_R * c) / (2.0 * RHO_R);
             nrr[r] = a + sqrt(a * a + mu_r * c / (2.0 * RHO_R));
             prr[r] = c + nrr[r];
@@ -863,6 +883,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 st.in_soft = 0;
                 st.soft_cnt = 0;
                 st.pend = GP_IDLE_RESTO;
+                st.iter--;  // the oracle starts the restoration phase in the iteration of the undone step
                 A.st[b] = st;
             }
             return;
@@ -990,7 +1011,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         gs[i] = g;
         rin[i] = cact(k, q) ? R(k)[D::O_CI + q] - s[i] + (rsm ? nrr[i] - prr[i] : 0.0) : 0.0;
     }
-    for (int e = lane; e < N * NX; e += 64) rdyn[e] = R(e / NX)[D::O_F + e % NX] - x[(e / NX + 1) * NX + e % NX];
+    for (int e = lane; e < N * NX; e += 64)
+        rdyn[e] = R(e / NX)[D::O_F + e % NX] - x[(e / NX + 1) * NX + e % NX] + (rlx ? nrr[NRD + e] - prr[NRD + e] : 0.0);
     for (int e = lane; e < N * NET; e += 64) {
         const int k = e / NET, ee = e % NET;
         double v = ee < NEA ? ((ee < NE && eqon(k)) ? R(k)[D::O_CE + ee] : 0.0) : R(k)[D::O_CM + ee - NEA];
@@ -1039,12 +1061,57 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
         for (int q = lane; q < NI; q += 64) acts[q] = cact(k, q) ? 1 : 0;
     };
+    // IPOPT's restoration problem puts elastic p, n on the dynamics rows too (oracle/mf_ocp.c ric_relax): row k reads
+    // dx_{k+1} = A dx_k + B du_k + r - D_r dlam_k, D_r = 1/Sp + 1/Sn.  With L = I + P_{k+1} D_r (LU, partial
+    // pivoting) the stage continues with P~ = L^-1 P_{k+1} (into Ps), J~^T = L^-1 J_n^T (Jts, node k+1's state
+    // rows) and the state-equality block -dc - J~ D_r J_n^T; G = I + S P S (S = D_r^1/2) must be positive definite
+    // for the eliminated (x_{k+1}, lam_k) pair to have the right inertia.  Hs is the scratch (W arrives after).
+    // Returns 1 for wrong inertia or a singular L (the inertia correction then raises delta_w).
+    auto relax_stage = [&](int k, bool en) __attribute__((always_inline)) -> int {
+        double *Gm = Hs, *Lm = Hs + NX * NX;
+        for (int j = lane; j < NX; j += 64) Drs[j] = rdiag(NRD + (size_t)k * NX + j);
+        __syncthreads();
+        for (int e = lane; e < NX * NX; e += 64) {
+            const int i = e / NX, j = e % NX;
+            const double id = (i == j) ? 1.0 : 0.0;
+            Gm[e] = id + sqrt(Drs[i]) * Ps[e] * sqrt(Drs[j]);
+            Lm[e] = id + Ps[e] * Drs[j];
+        }
+        __syncthreads();
+        const BKInertia gi = bk_factor_wave<NX>(Gm, NX, permx, pivx);
+        if (gi.zero || gi.neg) return 1;
+        if (lu_factor_wave<NX>(Lm, NX, pix)) return 1;
+        // lane c < NX: column c of P~ (into Gm, free now); lanes NX.. NX + NE - 1: the rows of J~
+        double y[NX];
+        if (lane < NX) {
+            lu_solve_lane<NX, NX>(Lm, pix, Ps + lane, NX, y);
+#pragma unroll
+            for (int i = 0; i < NX; i++) Gm[i * NX + lane] = y[i];
+        } else if (NE > 0 && en && lane < NX + NE) {
+            lu_solve_lane<NX, NX>(Lm, pix, R(k + 1) + D::O_JE + (lane - NX) * NX, 1, y);
+#pragma unroll
+            for (int i = 0; i < NX; i++) Jts[(lane - NX) * NX + i] = y[i];
+        }
+        __syncthreads();
+        for (int e = lane; e < NX * NX; e += 64) {
+            const int i = e / NX, j = e % NX;
+            Ps[e] = (i == j) ? Gm[e] : 0.5 * (Gm[i * NX + j] + Gm[j * NX + i]);
+        }
+        double *lu = A.LUg + b * Z.lu() + (size_t)k * (NX * NX + NX);
+        for (int e = lane; e < NX * NX; e += 64) lu[e] = Lm[e];
+        for (int e = lane; e < NX; e += 64) lu[NX * NX + e] = (double)pix[e];
+        if (en)
+            for (int e = lane; e < NE * NX; e += 64) A.Jtg[b * Z.jt() + (size_t)k * NEA * NX + e] = Jts[e];
+        __syncthreads();
+        return 0;
+    };
     auto factor = [&](double dw, double dc, double d1) __attribute__((always_inline)) -> int {
         for (int e = lane; e < NX * NX; e += 64) Ps[e] = (e / NX == e % NX) ? Sx[N * NX + e / NX] + dw : 0.0;
         __syncthreads();
         for (int k = N - 1; k >= 0; k--) {
             GSTAMP(2);
             const bool en = eqon(k + 1);
+            if (rlx && relax_stage(k, en)) return 1;
             for (int e = lane; e < NX * NX; e += 64) Pg[(size_t)k * NX * NX + e] = Ps[e];
             stage_in(k, true);
             for (int j = lane; j < NX; j += 64) Vs[V_SX + j] = Sx[k * NX + j];
@@ -1098,15 +1165,21 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (a < NU && c < NU) {
                     continue;  // the control block: tile_gemm above
                 } else if (a >= NU && c >= NU) {
-                    const int ee = a - NU;
+                    const int ee = a - NU, e2 = c - NU;
                     const size_t rr = NRo + (size_t)(ee >= NEA ? k : k + 1) * NET + ee;
                     v = (a == c) ? ((ee >= NEA || (en && ee < NE)) ? -dc - rdiag(rr) : -1.0) : 0.0;
+                    if (rlx && en && ee < NE && e2 < NE) {  // - J~ D_r J_n^T (elastic dynamics rows)
+                        double acc = 0.0;
+                        for (int l = 0; l < NX; l++) acc += Jts[ee * NX + l] * Drs[l] * Jn[e2 * NX + l];
+                        v -= acc;
+                    }
                 } else {
                     const int ee = (a >= NU ? a : c) - NU, uu = a >= NU ? c : a;
+                    const double *Jx = rlx ? Jts : Jn;
                     if (fixs[uu]) v = 0.0;
                     else if (ee >= NEA) v = JMs[(ee - NEA) * NV + NX + uu];  // mixed row of stage k
                     else if (en && ee < NE)
-                        for (int l = 0; l < NX; l++) v += Jn[ee * NX + l] * Bb[l * NU + uu];
+                        for (int l = 0; l < NX; l++) v += Jx[ee * NX + l] * Bb[l * NU + uu];
                 }
                 Ks[a * LDK + c] = v;
             }
@@ -1117,11 +1190,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             for (int e = NU * NX + lane; e < NK * NX; e += 64) {
                 const int a = e / NX, j = e % NX;
                 double v = 0.0;
+                const double *Jx = rlx ? Jts : Jn;
                 if (k > 0) {
                     if (a - NU >= NEA) {
                         v = JMs[(a - NU - NEA) * NV + j];
                     } else if (en && a - NU < NE) {
-                        for (int l = 0; l < NX; l++) v += Jn[(a - NU) * NX + l] * Ab[l * NX + j];
+                        for (int l = 0; l < NX; l++) v += Jx[(a - NU) * NX + l] * Ab[l * NX + j];
                     }
                 }
                 Rh[e] = v;
@@ -1201,7 +1275,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             const double *rk = R(k);
             const bool en = eqon(k + 1);
             GSTAMP(26);
-            for (int j = lane; j < NX; j += 64) pvg[k * NX + j] = pvs[j];
+            if (!rlx)
+                for (int j = lane; j < NX; j += 64) pvg[k * NX + j] = pvs[j];
             // every operand of the stage into LDS in one round trip: the record parts, P_{k+1} (T2),
             // the stored stage factorisation (Ks, perm, piv) and feedback (Kf), the stage vectors
             stage_in(k, false);
@@ -1220,6 +1295,11 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (k > 0) glds_copy(Vs + V_LP, lam + (k - 1) * NX, NX);
                 if (k + 1 < N) glds_copy(Vs + V_RN, re + (k + 1) * NET, NEA);
                 if (eqon(k) && NE > 0) glds_copy(Vs + V_JE, rk + D::O_JE, NE * NX);
+                if (rlx) {  // elastic dynamics rows: the stage's LU of I + P D_r and permutation, J~ (Hs rows < NX: free)
+                    glds_copy(Hs, A.LUg + b * Z.lu() + (size_t)k * (NX * NX + NX), NX * NX + NX);
+                    if (en && NE > 0) glds_copy(Jts, A.Jtg + b * Z.jt() + (size_t)k * NEA * NX, NE * NX);
+                    for (int j = lane; j < NX; j += 64) Drs[j] = rdiag(NRD + (size_t)k * NX + j);
+                }
                 for (int e = lane; e < NK; e += 64) {
                     perm[e] = (int)kst[NK * LDK + e];
                     piv[e] = (int)kst[NK * LDK + NK + e];
@@ -1236,6 +1316,21 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (k + 1 >= N) Vs[V_RN + ee] = 0.0;
             for (int e = lane; e < NEA * NX; e += 64)
                 if (!(eqon(k) && e < NE * NX)) Vs[V_JE + e] = 0.0;
+            if (rlx) {  // p~ = L^-1 p_{k+1} (stored for the forward sweep), rd + the elastic rows' correction
+                for (int j = lane; j < NX; j += 64) {
+                    pix[j] = (int)Hs[NX * NX + j];
+                    Vs[V_RD + j] += rowr[NRD + (size_t)k * NX + j];
+                }
+                wave_lds_sync();
+                if (lane == 0) {
+                    double y[NX];
+                    lu_solve_lane<NX, NX>(Hs, pix, pvs, 1, y);
+#pragma unroll
+                    for (int i = 0; i < NX; i++) ptv[i] = y[i];
+                }
+                wave_lds_sync();
+                for (int j = lane; j < NX; j += 64) pvg[k * NX + j] = ptv[j];
+            }
             // slack-row weights of the stage (vx: the J_I^T w term)
             for (int q = lane; q < NI; q += 64) {
                 const int i = k * NIA + q;
@@ -1268,7 +1363,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 vx[a] = g;
             }
             for (int j = lane; j < NX; j += 64) {
-                double acc = pvs[j];
+                double acc = rlx ? ptv[j] : pvs[j];
                 for (int l = 0; l < NX; l++) acc += T2[j * NX + l] * Vs[V_RD + l];
                 tv[j] = acc;
             }
@@ -1288,7 +1383,10 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                     const int ee = a - NU;
                     z = Vs[V_RN + ee];
                     if (rsm) z += rowr[NRo + (size_t)(k + 1) * NET + ee];
-                    for (int l = 0; l < NX; l++) z += Jn[ee * NX + l] * Vs[V_RD + l];
+                    if (rlx)  // J~ rh - J_n D_r p~
+                        for (int l = 0; l < NX; l++) z += Jts[ee * NX + l] * Vs[V_RD + l] - Jn[ee * NX + l] * Drs[l] * ptv[l];
+                    else
+                        for (int l = 0; l < NX; l++) z += Jn[ee * NX + l] * Vs[V_RD + l];
                 }
                 zv[a] = z;
                 duv[a] = -z;
@@ -1327,6 +1425,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             glds_copy(zv, kvg + k * NK, NK);
             glds_copy(tv, pvg + k * NX, NX);
             glds_copy(vx, rd + k * NX, NX);
+            if (rlx && en && NE > 0) glds_copy(Jts, A.Jtg + b * Z.jt() + (size_t)k * NEA * NX, NE * NX);
             for (int e = lane; e < NEA * NX; e += 64)
                 if (!(en && e < NE * NX)) Jn[e] = 0.0;
             for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
@@ -1338,6 +1437,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 duv[a] = acc;
                 if (a < NU) du[k * NU + a] = acc;
             }
+            double drj = 0.0, dlj = 0.0;  // (elastic dynamics rows) D_r and dlam of this lane's state j
+            if (rlx)
+                for (int j = lane; j < NX; j += 64) {
+                    vx[j] += rowr[NRD + (size_t)k * NX + j];
+                    drj = rdiag(NRD + (size_t)k * NX + j);
+                }
             gsync();
             for (int j = lane; j < NX; j += 64) {
                 double acc = vx[j];
@@ -1347,18 +1452,21 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             }
             gsync();
             for (int j = lane; j < NX; j += 64) {
+                // dlam = P~ z + p~ + J~^T dy_s, dx_{k+1} = z - D_r dlam (hard rows: P, p, J_n, D_r = 0)
                 double acc = tv[j];
                 for (int l = 0; l < NX; l++) acc += T2[j * NX + l] * dxn[l];
+                const double *Jx = rlx ? Jts : Jn;
                 if (en)
-                    for (int ee = 0; ee < NE; ee++) acc += Jn[ee * NX + j] * duv[NU + ee];
+                    for (int ee = 0; ee < NE; ee++) acc += Jx[ee * NX + j] * duv[NU + ee];
                 dlam[k * NX + j] = acc;
-                dx[(k + 1) * NX + j] = dxn[j];
+                dlj = acc;
+                dx[(k + 1) * NX + j] = rlx ? dxn[j] - drj * acc : dxn[j];
             }
             if (k + 1 < N)
                 for (int ee = lane; ee < NEA; ee += 64) dye[(k + 1) * NET + ee] = (en && ee < NE) ? duv[NU + ee] : 0.0;
             for (int m = lane; m < NM; m += 64) dye[k * NET + NEA + m] = duv[NU + NEA + m];
             gsync();
-            for (int j = lane; j < NX; j += 64) dxs[j] = dxn[j];
+            for (int j = lane; j < NX; j += 64) dxs[j] = rlx ? dxn[j] - drj * dlj : dxn[j];
             gsync();
         }
         GSTAMP(17);
@@ -1410,7 +1518,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         if (rsm)  // elastic variables: Sp dp = dy - r_p, Sn dn = -dy - r_n, and their bound multipliers
             for (int r = lane; r < NRI; r += 64) {
                 if (!el_on(r)) { dpr[r] = dnr[r] = dzp[r] = dzn[r] = 0.0; continue; }
-                const double dy = (size_t)r < NRo ? dyi[r] : dye[r - NRo], y = el_y(r);
+                const double dy = (size_t)r < NRo ? dyi[r] : ((size_t)r < NRD ? dye[r - NRo] : dlam[r - NRD]), y = el_y(r);
                 const double rp = RHO_R + gpr[r] - y, rn = RHO_R + gnr[r] + y;
                 dpr[r] = (dy - rp) / Spr[r];
                 dnr[r] = (-dy - rn) / Snr[r];
@@ -1496,7 +1604,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             GCHK_LANE((k << 8) | 2);
             if (!rsm) fs += l;
             for (int j = 0; j < NX; j++) {
-                const double r = f[j] - xx[(k + 1) * NX + j];
+                const size_t rr = NRD + (size_t)k * NX + j;
+                const double r = f[j] - xx[(k + 1) * NX + j] + (rlx ? ne_[rr] - pe[rr] : 0.0);
                 t += fabs(r);
                 if (trd) trd[k * NX + j] = r;
             }
@@ -1602,7 +1711,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     };
 
     if constexpr (PH == 1) {
-    if (flt && (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO)) return;
+    if (flt && (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO || st.pend == GP_WDSOFT)) return;
     // ---------------- inertia correction.  Merit mode: DESIGN.md section 4 (tiers).  IPOPT mode
     // (IpPDPerturbationHandler.cpp, oracle/mf_ocp.c factor_f): delta_w = 0 first; on wrong inertia 1e-4 if no
     // earlier perturbation, else max(1e-20, last / 3); then x100 (no earlier one, or last far below) or x8 up to
@@ -1678,8 +1787,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     // ================= IPOPT's FindAcceptableTrialPoint (oracle/mf_ocp.c ipm_filter / filter_backtrack)
     if (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO) {
         if (lane == 0) {
+            if (st.pend == GP_IDLE) st.iter++;  // (the restoration's exit ends an iteration; an undone soft step not)
             st.pend = st.pend == GP_IDLE_RESTO ? GP_RESTO : GP_NONE;
-            st.iter++;
             A.st[b] = st;
         }
         return;
@@ -1865,7 +1974,15 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     };
     bool want_soft = false, soft_entry = false, go_resto = false, do_step = false;
     double step_a = 0.0, step_az = 0.0;
-    if (m == 0 && st.in_soft) {  // soft restoration phase: at most max_soft_resto_iters = 10 iterations
+    if (st.pend == GP_WDSOFT) {
+        // the failed search after StopWatchDog, continued with the stored point's records: PrepareRestoPhaseStart
+        // (the filter takes the point, phc / thc evaluated there above), then the soft restoration phase
+        st.pend = GP_NONE;
+        st.n_ls_fail++;
+        fil_add(0, phc - 1e-8 * thc, (1.0 - 1e-5) * thc);
+        want_soft = true;
+        soft_entry = true;
+    } else if (m == 0 && st.in_soft) {  // soft restoration phase: at most max_soft_resto_iters = 10 iterations
         if (++st.soft_cnt <= 10) want_soft = true;
         else go_resto = true;
     } else {
@@ -1878,7 +1995,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         double rph = st.in_wd ? st.wd_ph : phc, rth = st.in_wd ? st.wd_th : thc, rgd = st.in_wd ? st.wd_gd : gdc;
         double alpha = ap, atest = ap, pht = 0.0, th_cur = thc;
         int n_steps = 0, soc_used = 0;
-        bool wd_step = false, accepted = false;
+        bool wd_step = false, accepted = false, wd_stopped = false;
         for (int pass = 0; pass < 2; pass++) {
             const bool inwd = pass == 0 && st.in_wd;
             accepted = backtrack(pass == 1, inwd, ap, th_cur, rph, rth, rgd, alpha, atest, n_steps, soc_used, pht, az);
@@ -1892,6 +2009,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 ftb(ap, az);
                 rph = st.wd_ph; rth = st.wd_th; rgd = st.wd_gd;
                 th_cur = INFINITY;  // (no second-order correction after a skipped first trial point)
+                wd_stopped = true;
                 continue;
             }
             accepted = true;  // the watchdog's full trial step, no filter update
@@ -1908,6 +2026,14 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             do_step = true;
             step_a = alpha;
             step_az = az;
+        } else if (wd_stopped && m == 0) {
+            // the records describe the abandoned watchdog point: re-evaluate at the restored one first (GP_WDSOFT)
+            if (lane == 0) {
+                st.pend = GP_WDSOFT;
+                st.mu = mu;
+                A.st[b] = st;
+            }
+            return;
         } else {
             st.n_ls_fail++;
             if (m == 1) { finish(GS_RESTOFAIL); return; }  // no restoration inside the restoration phase
@@ -1955,6 +2081,13 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         t[14] = st.pend; t[15] = st.in_soft;
     }
     if (do_step) apply_step(step_a, step_az);
+    if (go_resto) {  // the restoration phase starts within this iteration (oracle resto_phase): not counted here
+        if (lane == 0) {
+            st.mu = mu;
+            A.st[b] = st;
+        }
+        return;
+    }
     store();
     return;
     }  // flt
@@ -2138,6 +2271,17 @@ __global__ void k_gout(GArrays A, int N, int batch, double *w, int *status, int 
     }
 }
 
+// Continuous batching: every problem's status row starts as max_iter with no iterations, so a problem the host's launch
+// bound leaves unassigned to a slot reads as not converged (not as an uninitialised row)
+__global__ void k_gout_init(int total, int *status, int *iters, double *kkt, double *obj) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    if (status) status[i] = GS_MAXITER;
+    if (iters) iters[i] = 0;
+    if (kkt) kkt[i] = INFINITY;
+    if (obj) obj[i] = NAN;
+}
+
 // Continuous batching: a finished slot's solution goes to its problem's output row, and the slot takes the next
 // unsolved problem (x_0 and line reference staged into the slot; k_ginit initialises it).  force: the host's
 // launch bound was reached -- running slots are written out as max_iter and no problem is handed out.
@@ -2267,7 +2411,7 @@ template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **
              {&A.pr, Z.nr()}, {&A.nr, Z.nr()}, {&A.zp, Z.nr()}, {&A.zn, Z.nr()}, {&A.dpr, Z.nr()},
              {&A.dnr, Z.nr()}, {&A.dzp, Z.nr()}, {&A.dzn, Z.nr()}, {&A.tpr, Z.nr()}, {&A.tnr, Z.nr()},
              {&A.Sp, Z.nr()}, {&A.Sn, Z.nr()}, {&A.gp, Z.nr()}, {&A.gn, Z.nr()}, {&A.rowr, Z.nr()},
-             {&A.wR, Z.wv()}, {&A.dR, Z.wv()}};
+             {&A.wR, Z.wv()}, {&A.dR, Z.wv()}, {&A.LUg, Z.lu()}, {&A.Jtg, Z.jt()}};
 }
 
 static void gfree_ws(mf_gproblem *p) {
@@ -2335,6 +2479,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     P.warm_start = (o && d_w0) ? o->warm_start : 0;
     P.filter = o ? o->filter : 0;
     P.dbg = (o && o->verbose >= 2) ? 1 : 0;
+    P.resto_hard_dyn = o ? o->resto_hard_dyn : 0;
     p->last_batch = batch;
     // IPOPT bound_relax_factor: every finite bound of a non-fixed variable or row moves out by
     // br max(1, |b|) (oracle/mf_ocp.c, same rule); fixed controls (lo == hi) stay parameters
@@ -2381,6 +2526,8 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
         A.pidx = p->d_slots;
         A.init = p->d_slots + batch;
         A.next = p->d_slots + 2 * batch;
+        hipLaunchKernelGGL(k_gout_init, dim3((total + 255) / 256), dim3(256), 0, s, total, d_status, d_iters, d_kkt, d_obj);
+        GHIPCHK(hipGetLastError());
     }
     GHIPCHK(hipMemcpyAsync(A.x0, d_x0, sizeof(double) * D::NX * (size_t)batch, hipMemcpyDeviceToDevice, s));
     if (FAM::LREF != 2) {

@@ -7,8 +7,8 @@
   ipopt_mode_C3sf    C3 shared fatigue budget, N = 100, from the unperturbed G1 start
 
 each solved as the reference solves (Box_Pilz_6DOF.py:455-456, RepeatedMPCwithThermal.py:464-466): IPOPT from
-x0 = 0 with the filter globalisation (restoration with the dynamics rows exact, the device's variant) and
-bound_relax_factor 1e-8.  The perturbations are numpy default_rng(0) draws; each file holds the full decision
+x0 = 0 with the filter globalisation (IPOPT's restoration phase: elastic variables on every row, the dynamics rows
+included) and bound_relax_factor 1e-8, the KKT factored by the device's Riccati elimination (riccati = 2).  The perturbations are numpy default_rng(0) draws; each file holds the full decision
 vector w, whose first nx entries are the start x_0, so the GPU tests read the starts back from the fixtures.
 tests/test_gpu_generic.py compares the device against these (the hyper-dual oracle takes minutes per C3 horizon,
 too slow for the GPU box).
@@ -27,7 +27,8 @@ sys.path.insert(0, ROOT)
 
 from mpc_fatigue_amd import problems as PR  # noqa: E402
 
-IPOPT_MODE = dict(init_zero=True, bound_relax=1e-8, max_iter=1500, max_soc=4, filter=True, resto_hard_dyn=True)
+IPOPT_MODE = dict(init_zero=True, bound_relax=1e-8, max_iter=3000, max_soc=4, filter=True, resto_hard_dyn=False,
+                  riccati=2)
 
 
 def jobs():

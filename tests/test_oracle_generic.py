@@ -107,7 +107,7 @@ def test_box_resolve_matches_reference_trajectory(golden, name, kw):
     assert res[-1].cviol < 1e-8
 
 
-IPOPT_MODE = dict(init_zero=True, bound_relax=1e-8, max_iter=1500, max_soc=4, filter=True, resto_hard_dyn=True)
+IPOPT_MODE = dict(init_zero=True, bound_relax=1e-8, max_iter=1500, max_soc=4, filter=True)
 
 
 @pytest.mark.parametrize("name,kw", [("G1_box_N50", dict(N=50)), ("G4_box_N80", dict(N=80, right_const=False))])

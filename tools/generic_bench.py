@@ -140,7 +140,7 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
                "converged_frac": conv / batch, "seconds": dt, "stages": len(stages),
                "mean_iters_per_stage": [i / batch for i in its], "stage_max_iter": caps,
                "N": N, "nx": nx, "nu": nu, "ni": gs[0].ni}
-        if cpu and sample > 0 and name not in lrefs:
+        if cpu and sample > 0:
             from oracle import cpu_fast as CF
             from oracle import generic as G
             fk = CF.FastNodes(spec)
@@ -149,11 +149,14 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
             # the same stages and caps on one host thread per horizon, with the GPU's KKT algorithm (the Riccati
             # recursion, mfg_opts.riccati) and the product's node functions built for the host
             for st_spec, cap in zip(stages, caps):
-                specs = [dict(st_spec, q0=list(X[i, :len(spec["q0"])]), T0=list(X[i, len(spec["q0"]):]))
-                         for i in range(sample)]
+                if name in lrefs:  # chain family: the start and its own line reference
+                    specs = [dict(st_spec, q0=list(X[i]), line_ref=list(lrefs[name][i])) for i in range(sample)]
+                else:
+                    specs = [dict(st_spec, q0=list(X[i, :len(spec["q0"])]), T0=list(X[i, len(spec["q0"]):]))
+                             for i in range(sample)]
                 kwc = dict(kw, max_iter=cap, riccati=True, **fk.opts_kw())
                 if kw.get("filter"):
-                    kwc["resto_hard_dyn"] = True  # the device's restoration problem (exact dynamics rows)
+                    kwc["riccati"] = 2  # the device's elimination in IPOPT's restoration phase too (ric_relax)
                 res = [G.solve_batch([sp_], nthreads=1, L=CF.lib(), w0=(None if w is None else w[i]), **kwc)
                        for i, sp_ in enumerate(specs)]
                 w = np.vstack([r[0] for r in res])
