@@ -109,6 +109,43 @@ def cpu_baseline(spec_of, Q0, lrefs, opts, threads: int, sample_mt: int, sample_
     return rec, w_mt, st_mt
 
 
+def workload_plan(batch: int, c5: bool, world: int) -> tuple[int, str, str]:
+    """(horizons over all ranks, scaling label, workload prefix): by default every GPU solves its own `batch`
+    horizons (weak scaling); with --c5 `batch` is C5's total, sharded over the ranks."""
+    gB = batch if c5 else batch * world
+    return gB, ("strong" if c5 else "weak"), (f"C5: {gB} horizons in total over {world} GPU(s), " if c5 else "")
+
+
+class StepLoop:
+    """Steps in flight.  Consecutive steps are independent batched solves, each on its own slot (solver workspace,
+    stream, host thread), so the iteration tail of one step overlaps the bulk of the next; every step still solves
+    the whole shard.  solve(step, slot, nb, ev) runs one step on `slot` and returns when it is done, after waiting
+    for `ev` (the event of that slot's last gather, or None); gather(step, slot) collects a finished step's
+    solutions from the slot's buffers (N > 1: the RCCL gather to rank 0) and returns the event the slot's next solve
+    waits for, so a slot's outputs are not overwritten before their gather has read them and no slot waits for
+    another's work.  Steps finish, and are gathered, in order."""
+
+    def __init__(self, inflight: int, solve, gather=None):
+        self.inflight = max(1, inflight)
+        self.solve, self.gather = solve, gather
+        self.gathered = [None] * self.inflight
+
+    def run(self, K: int, nb: int, gather: bool = True, first: int = 0) -> None:
+        from concurrent.futures import ThreadPoolExecutor
+        n = self.inflight
+        with ThreadPoolExecutor(n) as ex:
+            futs = []
+            for s_ in range(K + n):
+                if s_ >= n:  # step s_ - n done: its slot is free (gather its solutions)
+                    futs[s_ - n].result()
+                    if gather and self.gather is not None:
+                        i = (s_ - n) % n
+                        self.gathered[i] = self.gather(first + s_ - n, i)
+                if s_ < K:
+                    i = s_ % n
+                    futs.append(ex.submit(self.solve, first + s_, i, nb, self.gathered[i]))
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,7 +198,7 @@ def main() -> int:
     spec = PR.pilz6_bench(N=N)
     ocp = OCP(spec)
     n = ocp.n
-    gB = args.batch if args.c5 else args.batch * world  # C5: a fixed total; default: --batch per GPU
+    gB, scaling, wl_prefix = workload_plan(args.batch, args.c5, world)  # C5: a fixed total; default: --batch per GPU
     lo, hi = shard_range(gB, world, rank)
     B = hi - lo
     Q0_all = PR.pilz6_batch_q0(gB, seed=0)
@@ -183,45 +220,35 @@ def main() -> int:
     ptrs = {k: v.data_ptr() for k, v in out.items()}
     opts = dict(tol=1e-8, constr_viol_tol=1e-8, max_iter=args.max_iter, mu_init=0.1, F_init=PR.BENCH_F_INIT)
 
-    # Steps in flight: consecutive steps are independent batched solves, each on its own solver
-    # workspace and HIP stream, driven by its own host thread (the solve's host loop polls its
-    # stream), so the iteration tail of one step -- few horizons left, latency-bound kernels --
-    # overlaps the bulk of the next.  Every step still solves the whole batch.
+    # Steps in flight (StepLoop): each slot is its own solver workspace, HIP stream and host thread (the
+    # solve's host loop polls its stream); every slot solves on a stream of its own (none on the default
+    # stream, where the N > 1 gathers run)
     inflight = max(1, args.inflight)
-    # every slot solves on a stream of its own (none on the default stream, where the N > 1 gathers run)
     slots = [(ocp, torch.cuda.Stream(dev), out, ptrs)]
     for _ in range(inflight - 1):
         ob = {k: torch.empty_like(v) for k, v in out.items()}
         slots.append((OCP(spec), torch.cuda.Stream(dev), ob, {k: v.data_ptr() for k, v in ob.items()}))
-    gathered = [None] * inflight  # event after the RCCL gather of each slot's last solutions
     torch.cuda.synchronize(dev)
 
-    def solve_on(i, nb=hi - lo):
+    def solve_on(step, i, nb=hi - lo, ev=None):
         torch.cuda.set_device(dev)  # the HIP device is per host thread
         o, st, ob, pt = slots[i]
-        # N > 1: the new solve must not overwrite this slot's previous solutions before their gather has
-        # read them; it waits for that gather alone, not for other slots' work
-        if gathered[i] is not None:
-            st.wait_event(gathered[i])
+        if ev is not None:  # this slot's previous solutions gathered (N > 1)
+            st.wait_event(ev)
         o.solve_dev(q0.data_ptr(), lref.data_ptr(), nb, pt, stream=st.cuda_stream, **opts)
         st.synchronize()
 
+    def gather_slot(step, i):
+        _, _, ob, _ = slots[i]
+        gather_solutions(ob["w"], ob["status"], rank, world, total=gB)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))  # the stream the gather ran on
+        return ev
+
+    loop = StepLoop(inflight, solve_on, gather_slot if world > 1 else None)
+
     def run_steps(K, nb=hi - lo):
-        from concurrent.futures import ThreadPoolExecutor
-        with ThreadPoolExecutor(inflight) as ex:
-            futs = []
-            for s_ in range(K + inflight):
-                if s_ >= inflight:  # step s_ - inflight done: its slot is free (gather its solutions)
-                    futs[s_ - inflight].result()
-                    if world > 1 and nb == hi - lo:
-                        i = (s_ - inflight) % inflight
-                        _, _, ob, _ = slots[i]
-                        gather_solutions(ob["w"], ob["status"], rank, world, total=gB)
-                        ev = torch.cuda.Event()
-                        ev.record(torch.cuda.current_stream(dev))  # the stream the gather ran on
-                        gathered[i] = ev
-                if s_ < K:
-                    futs.append(ex.submit(solve_on, s_ % inflight, nb))
+        loop.run(K, nb, gather=(nb == hi - lo))
 
     run_steps(max(args.warmup, inflight))  # every slot warm (workspace allocated)
     torch.cuda.synchronize(dev)
@@ -255,7 +282,7 @@ def main() -> int:
     timing_steps = args.steps
     if inflight > 1:
         ocp.timing(True)
-        solve_on(0)
+        solve_on(0, 0)
         torch.cuda.synchronize(dev)
         timing_steps = 1
     stats = ocp.kernel_stats()
@@ -335,8 +362,8 @@ def main() -> int:
     result = {
         "metric": METRIC, "value": value, "unit": "horizons/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "strong" if args.c5 else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-        "config": {"workload": (f"C5: {gB} horizons in total over {world} GPU(s), " if args.c5 else "") +
+        "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": wl_prefix +
                                f"pilz6_force N={N} (fatigue floor {PR.BENCH_FLOOR:g} Nm), {B} horizons per GPU, "
                                "q0 = IK + U(-0.05,0.05), line ref = fk(q0)",
                    "horizon_nodes": N, "batch_per_gpu": B, "global_batch": gB,

@@ -75,6 +75,8 @@ def lib():
         L.mfg_node_derivs.argtypes = [dp, dp, C.POINTER(GOCP), dp, dp, dp, dp, dp, dp, dp]
         L.mfg_ric_check_max.argtypes = [C.c_int]
         L.mfg_ric_check_max.restype = C.c_double
+        L.mfg_wdfail_count.argtypes = [C.c_int]
+        L.mfg_wdfail_count.restype = C.c_int
         _lib = L
     return _lib
 

@@ -1640,6 +1640,13 @@ static int factor_f(ws_t *S, double mu, double *ic_last, int *n_ic, double *ts) 
 /* riccati = 3 (test mode): in the restoration phase factor and solve both ways, keep the Riccati
  * direction, and record the largest difference of the primal-dual steps relative to their size */
 static double g_ric_check = 0.0;
+/* test hook: searches after StopWatchDog that failed (the re-evaluated stored point goes to the restoration) */
+static int g_wd_fail = 0;
+int mfg_wdfail_count(int reset) {
+    const int v = g_wd_fail;
+    if (reset) g_wd_fail = 0;
+    return v;
+}
 /* largest residual of the current step (dx, du, dlam, dye) in the unfactored KKT system (the rows kkt_factor
  * assembles: stationarity of the free x_k, u_k; dynamics; equality rows) */
 static double kkt_resid(const ws_t *S, const double *rdyn, const double *rin, const double *req) {
@@ -2117,6 +2124,12 @@ static int ipm_filter(ws_t *S, fst_t *F, int *it, fcount_t *C, const resto_ctx *
                               &okc, NULL, NULL, NULL);
                 accepted = filter_backtrack(S, &F->LS, mu, tau_fb, ap, thc, 1, 0, 0.0, &alpha, &az, &atest, &n_steps,
                                             &soc_used, &pht, &tht, C->ts);
+                if (!accepted) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+                    g_wd_fail++;
+                }
             } else {  /* the watchdog's full trial step, no filter update */
                 accepted = 1; wd_step = 1; alpha = ap; n_steps = 0;
             }

@@ -138,3 +138,84 @@ def test_shard_solve_gather_equals_single_process():
                            F_init=PR.BENCH_F_INIT)
     np.testing.assert_array_equal(np.array(W), w1)  # same horizons in the same order, bit for bit
     assert S == [r.status for r in R1]
+
+
+def _steploop_worker(rank, world, port, q, K, inflight):
+    """bench.py's own step loop (StepLoop: steps in flight on per-slot buffers, per-slot gather to rank 0 after each
+    step, the next solve on a slot waiting for that slot's gather event) at world size 2 on gloo, C5 as --c5 runs it
+    (8192 horizons in total, shard_range over the ranks).  A deterministic CPU stand-in replaces the device solve:
+    row i of step s is a function of (q0_i, s), written into the slot's own buffer by the slot's host thread."""
+    import threading
+
+    import numpy as np
+
+    import bench
+    from mpc_fatigue_amd import problems as PR
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    gB, scaling, prefix = bench.workload_plan(8192, True, world)
+    lo, hi = shard_range(gB, world, rank)
+    Q0 = torch.from_numpy(PR.pilz6_batch_q0(gB, seed=0)[lo:hi])
+    bufs = [{"w": torch.zeros((hi - lo, 7), dtype=torch.float64), "status": torch.zeros(hi - lo, dtype=torch.int32)}
+            for _ in range(inflight)]
+    busy = [threading.Lock() for _ in range(inflight)]
+    log = []
+
+    def solve(step, slot, nb, ev):
+        if ev is not None:
+            assert ev.is_set()  # this slot's previous solutions were gathered before it is overwritten
+        with busy[slot]:
+            b = bufs[slot]
+            b["w"][:, :6] = torch.sin(Q0 * (step + 1))
+            b["w"][:, 6] = step
+            b["status"][:] = step % 3
+
+    def gather(step, slot):
+        W, S = gather_solutions(bufs[slot]["w"], bufs[slot]["status"], rank, world, total=gB)
+        if rank == 0:
+            log.append((step, W.numpy().copy(), S.numpy().copy()))
+        ev = threading.Event()
+        ev.set()
+        return ev
+
+    loop = bench.StepLoop(inflight, solve, gather)
+    loop.run(inflight, hi - lo)                      # warm-up steps, gathered as the bench does
+    loop.run(K, hi - lo, first=inflight)             # the timed steps
+    loop.run(2, 1024, gather=False, first=100)       # the 1024-horizon shard figure: solves only, no gather
+    if rank == 0:
+        q.put((gB, scaling, prefix, hi - lo, [(s, W.tolist(), S.tolist()) for s, W, S in log]))
+    dist.destroy_process_group()
+
+
+def test_bench_step_loop_gloo_equals_single_process():
+    """bench.py's step loop at world size 2 (gloo): C5's 8192 horizons sharded 4096 + 4096, 4 steps in flight,
+    each finished step's per-slot solutions gathered to rank 0 in step order.  Every gathered result has the 8192
+    rows of a single-process run of that step, bit for bit, and the labels are C5's strong scaling."""
+    import numpy as np
+
+    from mpc_fatigue_amd import problems as PR
+
+    world, K, inflight = 2, 6, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_steploop_worker, args=(r, world, port, q, K, inflight)) for r in range(world)]
+    for p in procs:
+        p.start()
+    gB, scaling, prefix, shard0, log = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert (gB, scaling, shard0) == (8192, "strong", 4096)
+    assert prefix == "C5: 8192 horizons in total over 2 GPU(s), "
+    assert [s for s, _, _ in log] == list(range(inflight + K))  # every step gathered once, in order
+    Q0 = PR.pilz6_batch_q0(gB, seed=0)
+    for s, W, S in log:
+        W = np.array(W)
+        assert W.shape == (8192, 7)
+        np.testing.assert_array_equal(W[:, :6], torch.sin(torch.from_numpy(Q0) * (s + 1)).numpy())
+        assert (W[:, 6] == s).all() and S == [s % 3] * 8192
+    # the default (weak) workload: every GPU its own batch
+    import bench
+    assert bench.workload_plan(8192, False, 8) == (65536, "weak", "")
