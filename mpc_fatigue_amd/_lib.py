@@ -75,7 +75,7 @@ class GOpts(C.Structure):
                 ("mu_init", C.c_double), ("init_zero", C.c_int), ("F_init", C.c_double),
                 ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("verbose", C.c_int),
                 ("warm_start", C.c_int), ("filter", C.c_int), ("bound_relax", C.c_double),
-                ("resto_hard_dyn", C.c_int)]
+                ("resto_hard_dyn", C.c_int), ("inertia_spec", C.c_int)]
 
 
 class SolverOpts(C.Structure):

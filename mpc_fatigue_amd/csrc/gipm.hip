@@ -64,6 +64,13 @@ enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INER
 // of the restoration phase, a re-evaluation) advance no iteration.
 enum { GP_NONE = 0, GP_SOFT = 1, GP_RESTO = 2, GP_LSM = 3, GP_IDLE = 4, GP_IDLE_RESTO = 5, GP_WDSOFT = 6 };
 constexpr int GFCAP = 512;  // filter entries per filter (dominated entries are dropped as IPOPT does)
+// Concurrent inertia tries: IPOPT's inertia correction is a sequential search over delta_w (0, then last / 3 or 1e-4,
+// then x8 / x100 ...), one whole Riccati factorisation per try (2.3-2.5 per iteration on C3 / C4).  When at most
+// GSPEC_MAX horizons are running -- the tail, where each horizon's serial factorisations set the batch time and the
+// device is otherwise idle -- k_gspec factors the first GNSPEC candidates of that sequence at once, one wavefront
+// each, into storage of their own; k_gkkt then replays the sequential search and takes a try's result (and copies its
+// factors) wherever the parameters match exactly, so the outcome is the sequential one bit for bit.
+constexpr int GNSPEC = 4, GSPEC_MAX = 64;
 // diagnostic trace of horizon 0 in IPOPT mode (mf_gopts.verbose >= 2; mf_gdebug_trace): per iteration one row
 // from k_gpre (E_0 pieces, the restoration exit test) and one from k_gls (line search)
 constexpr int GDBG_ROWS = 4096, GDBG_W = 16;
@@ -82,6 +89,10 @@ struct GArrays {
     // IPOPT's restoration problem with elastic dynamics rows (oracle ric_relax): per stage the LU factor of
     // I + P_{k+1} D_r with its row permutation, and J~ = J_e,k+1 (I + D_r P_{k+1})^-1
     double *LUg, *Jtg;
+    // concurrent inertia tries (IPOPT mode, few horizons running; k_gspec): rows r = s * GNSPEC + t of the factor
+    // storage for try t of the s-th running horizon (slist[s]; spec_of[b] = s or -1), its result code and (dw, dc)
+    double *Psp, *Ksp, *Fsp, *LUsp, *Jtsp, *sdw, *sdc;
+    int *slist, *spec_of, *sres;
     const double *u_lo, *u_hi, *c_lo, *c_hi;  // shared, N x NU / N x NI
     double *x0, *lref;                        // per problem: NX, FAM::LREF (line reference / pose targets)
     const double *u0, *w0;                    // optional per-problem fixed u_0 values / warm start
@@ -486,10 +497,15 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     constexpr int NX = D::NX, NU = D::NU, NV = D::NV, NI = D::NI, NE = D::NE, NIA = D::NIA, NEA = D::NEA;
     constexpr int NM = D::NM, NET = D::NET;  // mixed rows c_m(x_k, u_k): multipliers at ye[k NET + NEA + m]
     constexpr int NK = NU + NET, LDK = NK + 1;
-    const int b = blockIdx.x, lane = threadIdx.x;
-    if (b >= batch) return;
+    const int lane = threadIdx.x;
+    // PH 3 (k_gspec): block s GNSPEC + t is try t of the s-th running horizon, with factor storage row blockIdx.x
+    const int b = PH == 3 ? (blockIdx.x < GNSPEC * GSPEC_MAX ? A.slist[blockIdx.x / GNSPEC] : -1) : (int)blockIdx.x;
+    if (b < 0 || b >= batch) return;
     GState st = A.st[b];
-    if (st.status != GS_RUNNING) return;
+    if (st.status != GS_RUNNING) {
+        if (PH == 3 && lane == 0) A.sres[blockIdx.x] = -1;
+        return;
+    }
     GCHK(1, 0);
     __shared__ GModels<FAM> Gm;
     if constexpr (PH == 2) {
@@ -558,6 +574,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     double *sdyn = A.sdyn + b * Z.l(), *sin_ = A.sin_ + b * Z.i(), *seq = A.seq + b * Z.e();
     double *tx = A.tx + b * Z.x(), *tu = A.tu + b * Z.u(), *ts = A.ts + b * Z.i();
     double *Pg = A.P + b * Z.P(), *Kg = A.Kinv + b * Z.Kinv(), *Fg = A.Kfb + b * Z.Kfb(), *pvg = A.pv + b * Z.l();
+    double *LUb = A.LUg + b * Z.lu(), *Jtb = A.Jtg + b * Z.jt();  // elastic-dynamics factors (restoration)
+    if constexpr (PH == 3) {  // a speculative try factors into its own storage row
+        const size_t r = blockIdx.x;
+        Pg = A.Psp + r * Z.P(); Kg = A.Ksp + r * Z.Kinv(); Fg = A.Fsp + r * Z.Kfb();
+        LUb = A.LUsp + r * Z.lu(); Jtb = A.Jtsp + r * Z.jt();
+    }
     double *kvg = A.kv + b * Z.kv();
     const double *ulo = A.u_lo, *uhi = A.u_hi, *clo = A.c_lo, *chi = A.c_hi;
     const double *lref = A.lref + FAM::LREF * b;
@@ -1097,11 +1119,11 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             const int i = e / NX, j = e % NX;
             Ps[e] = (i == j) ? Gm[e] : 0.5 * (Gm[i * NX + j] + Gm[j * NX + i]);
         }
-        double *lu = A.LUg + b * Z.lu() + (size_t)k * (NX * NX + NX);
+        double *lu = LUb + (size_t)k * (NX * NX + NX);
         for (int e = lane; e < NX * NX; e += 64) lu[e] = Lm[e];
         for (int e = lane; e < NX; e += 64) lu[NX * NX + e] = (double)pix[e];
         if (en)
-            for (int e = lane; e < NE * NX; e += 64) A.Jtg[b * Z.jt() + (size_t)k * NEA * NX + e] = Jts[e];
+            for (int e = lane; e < NE * NX; e += 64) Jtb[(size_t)k * NEA * NX + e] = Jts[e];
         __syncthreads();
         return 0;
     };
@@ -1296,8 +1318,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (k + 1 < N) glds_copy(Vs + V_RN, re + (k + 1) * NET, NEA);
                 if (eqon(k) && NE > 0) glds_copy(Vs + V_JE, rk + D::O_JE, NE * NX);
                 if (rlx) {  // elastic dynamics rows: the stage's LU of I + P D_r and permutation, J~ (Hs rows < NX: free)
-                    glds_copy(Hs, A.LUg + b * Z.lu() + (size_t)k * (NX * NX + NX), NX * NX + NX);
-                    if (en && NE > 0) glds_copy(Jts, A.Jtg + b * Z.jt() + (size_t)k * NEA * NX, NE * NX);
+                    glds_copy(Hs, LUb + (size_t)k * (NX * NX + NX), NX * NX + NX);
+                    if (en && NE > 0) glds_copy(Jts, Jtb + (size_t)k * NEA * NX, NE * NX);
                     for (int j = lane; j < NX; j += 64) Drs[j] = rdiag(NRD + (size_t)k * NX + j);
                 }
                 for (int e = lane; e < NK; e += 64) {
@@ -1425,7 +1447,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             glds_copy(zv, kvg + k * NK, NK);
             glds_copy(tv, pvg + k * NX, NX);
             glds_copy(vx, rd + k * NX, NX);
-            if (rlx && en && NE > 0) glds_copy(Jts, A.Jtg + b * Z.jt() + (size_t)k * NEA * NX, NE * NX);
+            if (rlx && en && NE > 0) glds_copy(Jts, Jtb + (size_t)k * NEA * NX, NE * NX);
             for (int e = lane; e < NEA * NX; e += 64)
                 if (!(en && e < NE * NX)) Jn[e] = 0.0;
             for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
@@ -1710,8 +1732,55 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         gsync();
     };
 
+    if constexpr (PH == 3) {
+    // ---------------- speculative inertia try t (IPOPT mode): the t-th delta_w of the search k_gkkt will make
+    const int t = blockIdx.x % GNSPEC;
+    if (!flt || lsm || st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO || st.pend == GP_WDSOFT) {
+        if (lane == 0) A.sres[blockIdx.x] = -1;
+        return;
+    }
+    double dw = 0.0;
+    if (t > 0) {
+        dw = (st.ic_last == 0.0) ? 1e-4 : fmax(1e-20, st.ic_last / 3.0);
+        for (int i = 1; i < t; i++) dw *= (st.ic_last == 0.0 || 1e5 * st.ic_last < dw) ? 100.0 : 8.0;
+    }
+    const double dc = P.dc_always ? 1e-8 * pow(mu, 0.25) : 0.0;
+    const int fr = factor(dw, dc, 0.0);
+    if (lane == 0) {
+        A.sres[blockIdx.x] = fr;
+        A.sdw[blockIdx.x] = dw;
+        A.sdc[blockIdx.x] = dc;
+    }
+    return;
+    }  // PH 3
+
     if constexpr (PH == 1) {
     if (flt && (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO || st.pend == GP_WDSOFT)) return;
+    // a try k_gspec has made with exactly these parameters: its result, and on success its factors copied in
+    const int srow = (flt && !lsm && A.spec_of) ? A.spec_of[b] : -1;
+    auto spec_try = [&](double dw_, double dc_, double d1_, int &fr_) __attribute__((always_inline)) -> bool {
+        if (srow < 0 || d1_ != 0.0) return false;
+        for (int t = 0; t < GNSPEC; t++) {
+            const size_t r = (size_t)srow * GNSPEC + t;
+            if (A.sres[r] < 0 || A.sdw[r] != dw_ || A.sdc[r] != dc_) continue;
+            fr_ = A.sres[r];
+            if (fr_ == 0) {
+                auto cp = [&](double *dst, const double *src, size_t n) __attribute__((always_inline)) {
+                    for (size_t e = lane; e < n; e += 64) dst[e] = src[e];
+                };
+                cp(Pg, A.Psp + r * Z.P(), Z.P());
+                cp(Kg, A.Ksp + r * Z.Kinv(), Z.Kinv());
+                cp(Fg, A.Fsp + r * Z.Kfb(), Z.Kfb());
+                if (rlx) {
+                    cp(LUb, A.LUsp + r * Z.lu(), Z.lu());
+                    cp(Jtb, A.Jtsp + r * Z.jt(), Z.jt());
+                }
+                gsync();
+            }
+            return true;
+        }
+        return false;
+    };
     // ---------------- inertia correction.  Merit mode: DESIGN.md section 4 (tiers).  IPOPT mode
     // (IpPDPerturbationHandler.cpp, oracle/mf_ocp.c factor_f): delta_w = 0 first; on wrong inertia 1e-4 if no
     // earlier perturbation, else max(1e-20, last / 3); then x100 (no earlier one, or last far below) or x8 up to
@@ -1728,7 +1797,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     const int max_tries = flt ? 200 : 60;
     for (int tries = 0; tries < max_tries; tries++) {
         GSTAMP_COUNT(20, 1);
-        const int fr = factor(dw, dc, d1);
+        int fr;
+        if (!spec_try(dw, dc, d1, fr)) fr = factor(dw, dc, d1);
         if (fr == 0) { factor_ok = true; break; }
         if (lsm) break;
         if (fr == 2 && dc == 0.0) { dc = 1e-8 * pow(mu, 0.25); continue; }
@@ -2237,6 +2307,28 @@ __global__ __launch_bounds__(64) void k_gkkt(const DevModel *M0, const DevModel 
                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
     giter_phase<FAM, 1, true>(M0, M1, F0, F1, P, A, batch);
 }
+template <class FAM>
+__global__ __launch_bounds__(64) void k_gspec(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
+    giter_phase<FAM, 3, true>(M0, M1, F0, F1, P, A, batch);
+}
+// the running horizons (at most GSPEC_MAX, the host's condition for launching k_gspec) listed for k_gspec
+__global__ __launch_bounds__(1024) void k_gspec_list(GArrays A, int batch) {
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (int b = threadIdx.x; b < batch; b += blockDim.x) {
+        int s = -1;
+        if (A.st[b].status == GS_RUNNING) {
+            s = atomicAdd(&cnt, 1);
+            if (s >= GSPEC_MAX) s = -1;
+            else A.slist[s] = b;
+        }
+        A.spec_of[b] = s;
+    }
+    __syncthreads();
+    for (int s = cnt + threadIdx.x; s < GSPEC_MAX; s += blockDim.x) A.slist[s] = -1;
+}
 template <class FAM, bool FLT>
 __global__ __launch_bounds__(64) void k_gls(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                             const DevFrame *F1, GParams P, GArrays A, int batch) {
@@ -2391,6 +2483,7 @@ struct mf_gproblem {
     GState *d_st = nullptr;
     int *d_active = nullptr;
     int *d_slots = nullptr;  // continuous batching: pidx (cap) | init (cap) | next (1)
+    std::vector<void *> sbufs;  // concurrent inertia tries: storage rows, result codes, horizon lists
 };
 
 template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **, size_t>> &items, GArrays &A) {
@@ -2417,6 +2510,8 @@ template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **
 static void gfree_ws(mf_gproblem *p) {
     for (double *b : p->bufs) (void)hipFree(b);
     p->bufs.clear();
+    for (void *b : p->sbufs) (void)hipFree(b);
+    p->sbufs.clear();
     if (p->d_st) (void)hipFree(p->d_st);
     if (p->d_active) (void)hipFree(p->d_active);
     if (p->d_slots) (void)hipFree(p->d_slots);
@@ -2447,6 +2542,26 @@ template <class FAM> static int gensure_ws(mf_gproblem *p, int batch, hipStream_
     GHIPCHK(hipMalloc(&p->d_st, sizeof(GState) * (size_t)batch));
     GHIPCHK(hipMalloc(&p->d_active, sizeof(int)));
     GHIPCHK(hipMalloc(&p->d_slots, sizeof(int) * (2 * (size_t)batch + 1)));
+    {  // concurrent inertia tries: GNSPEC x GSPEC_MAX factor-storage rows (k_gspec)
+        using D = typename FAM::D;
+        const GSz<D> Z(p->spec.N);
+        const size_t R = (size_t)GNSPEC * GSPEC_MAX;
+        std::pair<void **, size_t> sp[] = {{(void **)&A.Psp, R * Z.P() * 8},   {(void **)&A.Ksp, R * Z.Kinv() * 8},
+                                           {(void **)&A.Fsp, R * Z.Kfb() * 8}, {(void **)&A.LUsp, R * Z.lu() * 8},
+                                           {(void **)&A.Jtsp, R * Z.jt() * 8}, {(void **)&A.sdw, R * 8},
+                                           {(void **)&A.sdc, R * 8},           {(void **)&A.sres, R * 4},
+                                           {(void **)&A.slist, GSPEC_MAX * 4}, {(void **)&A.spec_of, (size_t)batch * 4}};
+        for (auto &it : sp) {
+            void *ptr = nullptr;
+            hipError_t he = hipMalloc(&ptr, it.second);
+            if (he != hipSuccess) {
+                gfree_ws(p);
+                return capi_fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
+            }
+            p->sbufs.push_back(ptr);
+            *it.first = ptr;
+        }
+    }
     A.st = p->d_st;
     A.active = p->d_active;
     A.u_lo = p->d_ulo;
@@ -2559,12 +2674,21 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     // some launches advance no iteration (the restoration phase's start and end), so the host bound is on
     // launches, with room for those, not on iterations
     const long max_launches = (2L * P.max_iter + 64) * (stream_mode ? (total + batch - 1) / batch + 1 : 1);
+    // concurrent inertia tries while few horizons run (IPOPT mode; mf_gopts.inertia_spec < 0: never)
+    const bool spec_ok = P.filter && !(o && o->inertia_spec < 0);
+    GArrays As = A;  // k_gkkt's view: spec_of set while k_gspec runs
     for (long it = 0; it < max_launches && active > 0; it += chunk) {
+        const bool spec = spec_ok && active <= GSPEC_MAX;
+        As.spec_of = spec ? A.spec_of : nullptr;
         for (int c = 0; c < chunk; c++) {
             hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
             hipLaunchKernelGGL(k_gasm<FAM>, dim3(rec_blocks), dim3(256), 0, s, P, A, batch);
             hipLaunchKernelGGL(k_gpre<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
-            hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            if (spec) {
+                hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch);
+                hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * GSPEC_MAX), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            }
+            hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
             if (P.filter) hipLaunchKernelGGL((k_gls<FAM, true>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             else hipLaunchKernelGGL((k_gls<FAM, false>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
         }

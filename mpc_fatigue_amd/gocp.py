@@ -155,13 +155,14 @@ class GOCP:
 
     def opts(self, tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, F_init=0.0,
              u_init=None, max_soc=4, verbose=False, warm_start=False, filter=False, bound_relax=0.0,
-             resto_hard_dyn=False):
+             resto_hard_dyn=False, inertia_spec=0):
         """mf_gopts; warm_start: IPOPT warm_start_init_point constants for a w0 start; filter: IPOPT's
         globalisation (filter line search, watchdog, soft restoration, restoration phase) instead of the
         l1-merit search; bound_relax: IPOPT's bound_relax_factor; resto_hard_dyn: the restoration problem without
-        elastic variables on the dynamics rows (the pre-round-5 variant; IPOPT's own restoration by default)."""
+        elastic variables on the dynamics rows (the pre-round-5 variant; IPOPT's own restoration by default);
+        inertia_spec: -1 turns off the concurrent inertia tries of the few-horizons tail (results are the same)."""
         o = _lib.GOpts(tol, constr_viol_tol, max_iter, mu_init, int(init_zero), F_init, None, max_soc, int(verbose),
-                       int(warm_start), int(filter), float(bound_relax), int(resto_hard_dyn))
+                       int(warm_start), int(filter), float(bound_relax), int(resto_hard_dyn), int(inertia_spec))
         if u_init is not None:
             o._u = np.ascontiguousarray(u_init, dtype=np.float64)
             o.u_init = _lib.dptr(o._u)

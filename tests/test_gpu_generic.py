@@ -521,3 +521,36 @@ def test_c2_ipopt_restoration_with_elastic_dynamics_rows():
             (i, int(r.iters[b]), m["iter"])
         dq = np.abs(g.q_traj(r.w[b]) - g.q_traj(w_or)).max()
         assert dq < (1e-6 if same else 0.02), (i, dq)
+
+
+@pytest.mark.parametrize("case", ["c3", "c4", "c2"])
+def test_concurrent_inertia_tries_equal_sequential_search(case):
+    """The tail mode of the IPOPT-mode solver (csrc/gipm.hip k_gspec): while at most 64 horizons run, the first four
+    delta_w candidates of IPOPT's inertia-correction search are factored concurrently, and k_gkkt replays the
+    sequential search over their results.  Every horizon's solve -- status, iteration count and solution -- is the
+    sequential search's bit for bit (bench starts of C3 shared budget / C4 Centauro / C2, restoration included)."""
+    import os
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    kw = dict(IPOPT_MODE, max_iter=3000)
+    lr = None
+    if case == "c3":
+        spec = PR.box_shared_fatigue(N=100, q0=_golden_q0_g1())
+        X = np.vstack([np.loadtxt(os.path.join(gdir, f"bench_c3_{i}.csv"), delimiter=",")[None, :24] for i in (0, 1)])
+    elif case == "c4":
+        spec = PR.centauro(N=50, T=2.0)
+        X = np.vstack([np.loadtxt(os.path.join(gdir, f"bench_c4_{i}.csv"), delimiter=",")[None, :28] for i in (0, 1)])
+    else:
+        from oracle import pin_np as P
+        from oracle.urdf_np import load_urdf_file
+        spec = PR.pilz6_bench(N=100)
+        ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
+        X = PR.pilz6_batch_q0(64, seed=0)[[41, 45, 2]]
+        lr = np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in X])
+    g = GOCP(spec)
+    X = np.ascontiguousarray(X)
+    r1 = g.solve(x0=X, line_ref=lr, inertia_spec=-1, **kw)
+    r2 = g.solve(x0=X, line_ref=lr, **kw)
+    print(case, "sequential", r1.status.tolist(), r1.iters.tolist(), "concurrent", r2.status.tolist(), r2.iters.tolist())
+    np.testing.assert_array_equal(r2.status, r1.status)
+    np.testing.assert_array_equal(r2.iters, r1.iters)
+    np.testing.assert_array_equal(r2.w, r1.w)

@@ -1,7 +1,8 @@
 """Diagnostic: per-phase cycle shares of the generic solver's k_giter (build with -DMF_GSTAMPS:
 mpc_fatigue_amd/libmpcfatigue_gstamps.so, `make -C mpc_fatigue_amd libmpcfatigue_gstamps.so`).
 
-Usage: python tools/gdiag_stamps.py [batch] [iters] [case]    case: c3 (shared budget, pos_toll 1) | c4
+Usage: python tools/gdiag_stamps.py [batch] [iters] [case] [mode]    case: c3 (shared budget, pos_toll 1) | c4;
+mode: merit (default) | ipopt (x0 = 0, filter globalisation, the reference problem at pos_toll 1e-4)
 Slots: 0 opt-error+mu, 1 barrier/residuals, 2 factor rest, 8 stage loads, 9 H assembly, 10 PB / PA,
 11 stage block, 12 BK factor, 13 BK solve + stores, 14 P update; direction (both calls): 19 stage loads,
 23 vx / tv, 24 zv, 25 solve, 26 pvs and loop top, 17 forward sweep, 18 slack rows and bound multipliers; 3 rest, 4 ftb+merit0+gdot/pHp,
@@ -36,6 +37,9 @@ else:
     q0 = np.asarray(spec["q0"])
     X = np.hstack([q0[None] + rng.uniform(-0.02, 0.02, (B, 14)), np.tile(spec["T0"], (B, 1))])
     kw = dict(u_init=PR.centauro_u_init(spec), max_soc=4)
+if len(sys.argv) > 4 and sys.argv[4] == "ipopt":
+    spec = dict(spec, pos_toll=1e-4) if case == "c3" else spec
+    kw = dict(init_zero=True, filter=True, bound_relax=1e-8, max_soc=4)
 g = GOCP(spec)
 L = _lib.lib()
 g.solve(x0=X, max_iter=1, **kw)  # warm-up
