@@ -529,6 +529,55 @@ __device__ __forceinline__ int lu_factor_wave(double *M, int n, int *pi) {
     return 0;
 }
 
+// lu_factor_wave with the matrix in registers (compile-time M <= 64): lane r keeps original row r for the whole
+// factorisation and `at` = the position it has reached (the oracle swaps whole rows; here only positions move).  At
+// column c the pivot is the row of largest |value| among positions >= c, the smallest position among ties (the
+// sequential scan's choice); its values reach the other lanes by v_readlane, and the rows at positions > c take the
+// multiplier and the update in the same order as lu_factor_wave.  Writes the factor to M (row `at` of lane r) and pi
+// (pi[at] = r); returns 1 on an exactly zero pivot column (M, pi then unwritten).
+template <int LD, int M>
+__device__ __forceinline__ int lu_factor_regs(double *Mat, int *pi) {
+    static_assert(M <= 64, "one row per lane");
+    const int lane = lane_opaque();
+    const bool act = lane < M;
+    double a[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) a[j] = Mat[min(lane, M - 1) * LD + j];
+    int at = lane;
+    int sing = 0;
+#pragma unroll
+    for (int c = 0; c < M; c++) {
+        double v = (act && at >= c) ? fabs(a[c]) : -1.0;
+        int idx = (act && at >= c) ? at : 64;
+        wave_argmax(v, idx);  // idx: the pivot row's position
+        const unsigned long long bal = __ballot(act && at == idx);
+        const int pl = __builtin_ffsll((long long)bal) - 1;  // its lane
+        const double p = readlane_d(a[c], pl);
+        if (p == 0.0) sing = 1;
+        if (sing) break;
+        // the rows at positions c and idx trade places
+        if (act && at == c) at = idx;
+        else if (act && lane == pl) at = c;
+        double pr[M];  // the pivot row, broadcast (wave-uniform)
+#pragma unroll
+        for (int j = c + 1; j < M; j++) pr[j] = readlane_d(a[j], pl);
+        if (act && at > c) {
+            const double f = a[c] / p;
+            a[c] = f;
+#pragma unroll
+            for (int j = c + 1; j < M; j++) a[j] -= f * pr[j];
+        }
+    }
+    if (sing) return 1;
+    if (act) {
+#pragma unroll
+        for (int j = 0; j < M; j++) Mat[at * LD + j] = a[j];
+        pi[at] = lane;
+    }
+    wave_lds_sync();
+    return 0;
+}
+
 // y = (LU)^-1 b for the calling lane's right-hand side, b_i = b[pi[i] * bs] (the interchanges applied), in
 // registers: the unit-lower sweep by columns, then the upper one (oracle/mf_ocp.c lu_solve, same order)
 template <int LD, int M>

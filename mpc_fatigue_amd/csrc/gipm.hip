@@ -35,7 +35,8 @@ namespace mf {
 struct GState {
     double mu, nu, reg_last, E0, cviol, obj;
     double dw_c, dc_c;  // the regularisation the accepted factorisation was made with (k_gkkt -> k_gls)
-    int reg_tier, status, iter, n_ls_fail, n_ic, consec_fail, n_soc, pad;
+    int reg_tier, status, iter, n_ls_fail, n_ic, consec_fail, n_soc;
+    int frow;  // >= 0: this iteration's factors are k_gspec's storage row frow (k_gkkt -> k_gls), -1: the horizon's own
     // IPOPT mode (GParams::filter; the same algorithm as oracle/mf_ocp.c mfg_opts.filter with resto_hard_dyn)
     double ic_last, ic_last_main;  // last nonzero inertia perturbation: current problem / main problem in a restoration
     double thm[2][2];              // theta_max / theta_min of the main / restoration filter (< 0: unset)
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         GState st;
         st.mu = P.mu_init; st.nu = 0.0; st.reg_last = 0.0; st.E0 = INFINITY; st.cviol = INFINITY; st.obj = 0.0;
         st.reg_tier = 0; st.status = GS_RUNNING; st.iter = 0; st.n_ls_fail = 0; st.n_ic = 0; st.consec_fail = 0;
-        st.n_soc = 0; st.pad = 0; st.dw_c = 0.0; st.dc_c = 0.0;
+        st.n_soc = 0; st.frow = -1; st.dw_c = 0.0; st.dc_c = 0.0;
         st.ic_last = st.ic_last_main = 0.0;
         st.thm[0][0] = st.thm[0][1] = st.thm[1][0] = st.thm[1][1] = -1.0;
         st.rs_ph = st.rs_th = st.mu_orig = st.zeta = 0.0;
@@ -575,10 +576,15 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     double *tx = A.tx + b * Z.x(), *tu = A.tu + b * Z.u(), *ts = A.ts + b * Z.i();
     double *Pg = A.P + b * Z.P(), *Kg = A.Kinv + b * Z.Kinv(), *Fg = A.Kfb + b * Z.Kfb(), *pvg = A.pv + b * Z.l();
     double *LUb = A.LUg + b * Z.lu(), *Jtb = A.Jtg + b * Z.jt();  // elastic-dynamics factors (restoration)
-    if constexpr (PH == 3) {  // a speculative try factors into its own storage row
-        const size_t r = blockIdx.x;
+    // a speculative try factors into its own storage row (PH 3); the line search's second-order corrections solve
+    // with the factors k_gkkt took from such a row (PH 2, st.frow)
+    auto use_row = [&](size_t r) __attribute__((always_inline)) {
         Pg = A.Psp + r * Z.P(); Kg = A.Ksp + r * Z.Kinv(); Fg = A.Fsp + r * Z.Kfb();
         LUb = A.LUsp + r * Z.lu(); Jtb = A.Jtsp + r * Z.jt();
+    };
+    if constexpr (PH == 3) use_row(blockIdx.x);
+    if constexpr (PH == 2) {
+        if (P.filter && st.frow >= 0) use_row((size_t)st.frow);
     }
     double *kvg = A.kv + b * Z.kv();
     const double *ulo = A.u_lo, *uhi = A.u_hi, *clo = A.c_lo, *chi = A.c_hi;
@@ -1100,9 +1106,12 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             Lm[e] = id + Ps[e] * Drs[j];
         }
         __syncthreads();
-        const BKInertia gi = bk_factor_wave<NX>(Gm, NX, permx, pivx);
+        // (register factorisations where they give the LDS routines' results: natural-order Bunch-Kaufman for G,
+        // the row-per-lane LU for L)
+        BKInertia gi;
+        if (!bk_factor_regs<NX, NX>(Gm, permx, pivx, gi)) gi = bk_factor_wave<NX>(Gm, NX, permx, pivx);
         if (gi.zero || gi.neg) return 1;
-        if (lu_factor_wave<NX>(Lm, NX, pix)) return 1;
+        if (lu_factor_regs<NX, NX>(Lm, pix)) return 1;
         // lane c < NX: column c of P~ (into Gm, free now); lanes NX.. NX + NE - 1: the rows of J~
         double y[NX];
         if (lane < NX) {
@@ -1756,8 +1765,10 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
 
     if constexpr (PH == 1) {
     if (flt && (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO || st.pend == GP_WDSOFT)) return;
-    // a try k_gspec has made with exactly these parameters: its result, and on success its factors copied in
+    // a try k_gspec has made with exactly these parameters: its result, and on success the direction (and the line
+    // search's corrections, st.frow) use its factors where they lie
     const int srow = (flt && !lsm && A.spec_of) ? A.spec_of[b] : -1;
+    st.frow = -1;
     auto spec_try = [&](double dw_, double dc_, double d1_, int &fr_) __attribute__((always_inline)) -> bool {
         if (srow < 0 || d1_ != 0.0) return false;
         for (int t = 0; t < GNSPEC; t++) {
@@ -1765,17 +1776,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             if (A.sres[r] < 0 || A.sdw[r] != dw_ || A.sdc[r] != dc_) continue;
             fr_ = A.sres[r];
             if (fr_ == 0) {
-                auto cp = [&](double *dst, const double *src, size_t n) __attribute__((always_inline)) {
-                    for (size_t e = lane; e < n; e += 64) dst[e] = src[e];
-                };
-                cp(Pg, A.Psp + r * Z.P(), Z.P());
-                cp(Kg, A.Ksp + r * Z.Kinv(), Z.Kinv());
-                cp(Fg, A.Fsp + r * Z.Kfb(), Z.Kfb());
-                if (rlx) {
-                    cp(LUb, A.LUsp + r * Z.lu(), Z.lu());
-                    cp(Jtb, A.Jtsp + r * Z.jt(), Z.jt());
-                }
-                gsync();
+                use_row(r);
+                st.frow = (int)r;
             }
             return true;
         }

@@ -110,6 +110,21 @@ def generic_extra(batch: int = 1024, sample: int = 2, cpu: bool = True, seed: in
                  "obj": torch.empty(batch, dtype=torch.float64, device=dev)} for _ in stages]
 
         def run(label, max_iter=None):
+            import threading
+            done = threading.Event()
+
+            def heartbeat():  # a long batch solve prints nothing for minutes (gpurun's silence guard)
+                t_hb = time.perf_counter()
+                while not done.wait(30.0):
+                    print(f"[generic_bench] {name} {label}: running {time.perf_counter() - t_hb:.0f}s", file=sys.stderr,
+                          flush=True)
+            threading.Thread(target=heartbeat, daemon=True).start()
+            try:
+                _run(label, max_iter)
+            finally:
+                done.set()
+
+        def _run(label, max_iter=None):
             prev = None
             for i, (g, ob) in enumerate(zip(gs, bufs)):
                 ptr = {k: v.data_ptr() for k, v in ob.items()}
@@ -183,9 +198,14 @@ if __name__ == "__main__":
     ap.add_argument("--caps", default="", help="comma list of C3 homotopy stage iteration caps (default 1000 each)")
     ap.add_argument("--mode", default="ipopt", choices=["ipopt", "merit"])
     ap.add_argument("--slots", type=int, default=0, help="continuous batching: concurrent solves (0: the whole batch)")
+    ap.add_argument("--max-iter", type=int, default=0, help="iteration cap (0: IPOPT's default 3000)")
+    ap.add_argument("--no-spec", action="store_true", help="sequential inertia tries only (mf_gopts.inertia_spec = -1)")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
     caps = [int(c) for c in a.caps.split(",")] if a.caps else None
+    if a.no_spec:
+        IPOPT_KW["inertia_spec"] = -1
     print(json.dumps(generic_extra(a.batch, a.sample, cases=tuple(a.cases.split(",")), stage_caps=caps, mode=a.mode,
+                                   max_iter=a.max_iter,
                                    slots=a.slots)))
