@@ -40,11 +40,12 @@ def test_oracle_c_asan_ubsan():
     subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "asan"], stdout=subprocess.DEVNULL)
     libasan = subprocess.check_output(["gcc", "-print-file-name=libasan.so"], text=True).strip()
     assert os.path.exists(libasan)
-    # the IPOPT-mode code (filter, watchdog, soft restoration, restoration phase) runs under the sanitizers
-    # through the G1 cold solve (N = 50, restoration phases included); G4 and G3 repeat the same code at
-    # N = 80 and would take the child past its time limit at ASan speed
-    _child(["tests/test_oracle_golden.py", "tests/test_oracle_generic.py", "-k",
-            "not resolve_matches_reference_trajectory and not G4_box_N80 and not g3_ipopt_mode"],
+    # the IPOPT-mode code (filter, watchdog, soft restoration, IPOPT's restoration phase with elastic dynamics rows,
+    # the Riccati recursion through them and the banded factorisation of the same system) runs under the sanitizers
+    # through the C2 restoration check (test_oracle_resto_riccati, riccati = 3); the box cold solves repeat the same
+    # code at 400-550 iterations and would take the child past its time limit at ASan speed
+    _child(["tests/test_oracle_golden.py", "tests/test_oracle_generic.py", "tests/test_oracle_resto_riccati.py", "-k",
+            "not resolve_matches_reference_trajectory and not ipopt_mode and not hard_dynamics"],
            {"LD_PRELOAD": libasan, "MF_ORACLE_LIB": os.path.join(ROOT, "oracle", "_asan", "libmforacle.so")})
 
 
