@@ -269,6 +269,10 @@ int mf_gnode_record(mf_gproblem *p, const double *xu, const double *yi, const do
 /* Diagnostics: dual state of problem b after the last solve, [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU |
  * mu] (per-node blocks as the solver stores them).  Returns the number of doubles written. */
 int mf_gdebug_duals(mf_gproblem *p, int b, double *out);
+/* Diagnostics: solver counters of problem b after the last solve, out[10] = {iterations, status, inertia corrections,
+ * line-search failures, second-order-correction steps, restoration phases, watchdog starts, soft-restoration steps,
+ * failed searches after StopWatchDog, restoration-phase iterations}.  Returns 10. */
+int mf_gdebug_counters(mf_gproblem *p, int b, int *out);
 /* Diagnostics: IPOPT-mode trace of horizon 0 of the last solve made with opts.verbose >= 2, 2 x 4096 rows of 16
  * doubles (rows of the phase-0 kernel, then of the line-search kernel, indexed by iteration); returns 4096.
  * _reset zeroes it. */

@@ -131,6 +131,7 @@ def lib() -> C.CDLL:
                                  C.c_int),
         "mf_gnode_record": ([vp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
         "mf_gdebug_duals": ([vp, C.c_int, dp], C.c_int),
+        "mf_gdebug_counters": ([vp, C.c_int, ip], C.c_int),
         "mf_gdebug_trace": ([dp], C.c_int),
         "mf_gdebug_trace_reset": ([], C.c_int),
         "mf_last_error": ([], cp),
@@ -151,7 +152,7 @@ EXPORTED_SYMBOLS = [
     "mf_problem_kernel_stats", "mf_problem_trace", "mf_kernel_name", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
     "mf_gproblem_create", "mf_gproblem_free", "mf_gproblem_dims", "mf_gsolve_batch", "mf_gsolve_batch_dev",
     "mf_gsolve_stream_dev",
-    "mf_gnode_record", "mf_gdebug_duals", "mf_gdebug_trace", "mf_gdebug_trace_reset",
+    "mf_gnode_record", "mf_gdebug_duals", "mf_gdebug_counters", "mf_gdebug_trace", "mf_gdebug_trace_reset",
 ]
 
 

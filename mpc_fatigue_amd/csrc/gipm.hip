@@ -48,6 +48,7 @@ struct GState {
     int pend;                      // GP_*: pending action of the next phases
     int nf[2];                     // filter entries (main, restoration)
     int in_wd, wd_short, wd_trial, in_soft, soft_cnt, n_resto, n_wd, n_soft;
+    int n_wdfail, n_rit;  // failed searches after StopWatchDog (GP_WDSOFT rounds), restoration-phase iterations
 };
 enum { GS_RUNNING = -1, GS_CONVERGED = 0, GS_MAXITER = 1, GS_LSFAIL = 2, GS_INERTIA = 3, GS_RESTOFAIL = 4,
        GS_LOCINF = 5 };
@@ -479,6 +480,7 @@ __global__ __launch_bounds__(64) void k_ginit(const DevModel *M0, const DevModel
         st.wd_ph = st.wd_th = st.wd_gd = st.wd_atest = st.pd_cur = 0.0;
         st.mode = 0; st.pend = GP_NONE; st.nf[0] = st.nf[1] = 0;
         st.in_wd = st.wd_short = st.wd_trial = st.in_soft = st.soft_cnt = st.n_resto = st.n_wd = st.n_soft = 0;
+        st.n_wdfail = st.n_rit = 0;
         A.st[b] = st;
         if (A.init) A.init[b] = 0;
     }
@@ -1920,6 +1922,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     };
     auto store = [&]() __attribute__((always_inline)) {
         if (lane == 0) {
+            if (m == 1) st.n_rit++;
             st.iter++;
             st.mu = mu;
             A.st[b] = st;
@@ -2102,6 +2105,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             // the records describe the abandoned watchdog point: re-evaluate at the restored one first (GP_WDSOFT)
             if (lane == 0) {
                 st.pend = GP_WDSOFT;
+                st.n_wdfail++;
                 st.mu = mu;
                 A.st[b] = st;
             }
@@ -3043,6 +3047,22 @@ extern "C" int mf_gdebug_chk_dump(void) {
     return MF_OK;
 }
 #endif
+
+// diagnostics: the solver counters of problem b after the last solve (IPOPT mode): iterations, status, inertia
+// corrections, line-search failures, second-order-correction steps, restoration phases, watchdog starts,
+// soft-restoration steps, failed searches after StopWatchDog, restoration-phase iterations
+extern "C" int mf_gdebug_counters(mf_gproblem *p, int b, int *out) {
+    if (!p || !out) return capi_fail(MF_ERR_ARG, "null argument");
+    if (b < 0 || b >= p->last_batch || !p->d_st) return capi_fail(MF_ERR_ARG, "no such problem in the last solve");
+    int e = capi_ensure_device();
+    if (e) return e;
+    GState st;
+    GHIPCHK(hipMemcpy(&st, p->d_st + b, sizeof st, hipMemcpyDeviceToHost));
+    const int v[10] = {st.iter, st.status, st.n_ic, st.n_ls_fail, st.n_soc, st.n_resto, st.n_wd, st.n_soft,
+                       st.n_wdfail, st.n_rit};
+    for (int i = 0; i < 10; i++) out[i] = v[i];
+    return 10;
+}
 
 extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {
     if (!p || !out) return capi_fail(MF_ERR_ARG, "null argument");

@@ -246,6 +246,15 @@ class GOCP:
             w = r.w
         return stages[-1], stages
 
+    COUNTERS = ("iterations", "status", "inertia_corrections", "ls_failures", "soc_steps", "resto_phases",
+                "watchdog_starts", "soft_resto_steps", "wd_failed_searches", "resto_iterations")
+
+    def counters(self, b: int = 0) -> dict:
+        """Solver counters of problem b after the last solve (mf_gdebug_counters)."""
+        out = np.zeros(10, np.int32)
+        _lib.check(_lib.lib().mf_gdebug_counters(self._h, int(b), _lib.iptr(out)))
+        return dict(zip(self.COUNTERS, (int(v) for v in out)))
+
     def q_traj(self, w: np.ndarray) -> np.ndarray:
         """State trajectory x_0..x_N (N+1, nx) of a solution vector."""
         nx, nu, N = self.nx, self.nu, self.N

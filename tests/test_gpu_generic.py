@@ -554,3 +554,29 @@ def test_concurrent_inertia_tries_equal_sequential_search(case):
     np.testing.assert_array_equal(r2.status, r1.status)
     np.testing.assert_array_equal(r2.iters, r1.iters)
     np.testing.assert_array_equal(r2.w, r1.w)
+
+
+def test_watchdog_stop_with_failed_search_matches_oracle():
+    """A failed backtracking search after StopWatchDog (IPOPT's watchdog: the stored point and direction restored,
+    the search from alpha_max / 2 fails): the oracle re-evaluates the stored point before it augments the filter and
+    starts the soft restoration (oracle/mf_ocp.c ipm_filter), the device spends a GP_WDSOFT round on the same
+    re-evaluation (csrc/gipm.hip).  Start 13 of the C3 shared-budget bench draw takes that path once in
+    the oracle's IPM (tools/watchdog_scan.py; fixture tests/golden/ipopt_mode_C3_wd13.*, the oracle's IPM with the
+    product's node functions): the device's solve takes it too and ends at the oracle's solution."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from watchdog_scan import spec_of
+    gdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    meta = json.load(open(os.path.join(gdir, "ipopt_mode_C3_wd13.json")))
+    w_or = np.loadtxt(os.path.join(gdir, "ipopt_mode_C3_wd13.csv"), delimiter=",")
+    spec = spec_of("c3", 13)
+    g = GOCP(spec)
+    r = g.solve(x0=np.r_[spec["q0"], spec["T0"]][None], **dict(IPOPT_MODE, max_iter=3000))
+    cnt = g.counters(0)
+    print("device", int(r.status[0]), int(r.iters[0]), float(r.obj[0]), cnt, "oracle", meta)
+    assert int(r.status[0]) == 0
+    assert cnt["wd_failed_searches"] >= 1
+    assert abs(float(r.obj[0]) - meta["obj"]) <= 1e-6 * abs(meta["obj"])
+    assert np.abs(g.q_traj(r.w[0]) - g.q_traj(w_or)).max() < 1e-4
