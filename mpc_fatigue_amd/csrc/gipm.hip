@@ -2105,6 +2105,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             // the records describe the abandoned watchdog point: re-evaluate at the restored one first (GP_WDSOFT)
             if (lane == 0) {
                 st.pend = GP_WDSOFT;
+                st.frow = -1;  // (the next round's k_gspec may reuse this round's storage rows)
                 st.n_wdfail++;
                 st.mu = mu;
                 A.st[b] = st;
