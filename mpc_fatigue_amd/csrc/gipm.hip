@@ -2304,13 +2304,22 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     }
 }
 
+// k_gkkt's occupancy variant for full launches.  The chain families' stage arrays take ~6 KB of LDS, so their
+// k_gkkt is register-limited: at the default allocation (152 VGPRs) a CU holds 12 horizons and a 4096-horizon
+// launch runs in two rounds of waves that are latency-bound (lone and fully loaded waves take nearly the same
+// cycles per stage).  Capped at 128 VGPRs (4 waves per SIMD, some spills) the whole launch is resident: the
+// host takes this variant while many horizons run, the default one (no spills, faster lone waves) in the tail.  The box and Centauro families are LDS-limited (~50 KB: three
+// horizons per CU) and have only the default.
+template <class FAM> struct GOcc { static constexpr int KKT = 1; };
+template <int NJ, int NF, int NE, bool TH> struct GOcc<ChainFam<NJ, NF, NE, TH>> { static constexpr int KKT = 4; };
+
 template <class FAM>
 __global__ __launch_bounds__(64) void k_gpre(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
     giter_phase<FAM, 0, true>(M0, M1, F0, F1, P, A, batch);
 }
-template <class FAM>
-__global__ __launch_bounds__(64) void k_gkkt(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+template <class FAM, int OCC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_gkkt(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
     giter_phase<FAM, 1, true>(M0, M1, F0, F1, P, A, batch);
 }
@@ -2684,6 +2693,16 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     // concurrent inertia tries while few horizons run (IPOPT mode; mf_gopts.inertia_spec < 0: never)
     const bool spec_ok = P.filter && !(o && o->inertia_spec < 0);
     GArrays As = A;  // k_gkkt's view: spec_of set while k_gspec runs
+    // the occupancy variant while more than four horizons per CU run (measured crossover on the C2 leg: launches
+    // at ~1000 running horizons take the same time with either variant, fewer run faster without spills)
+    int kkt_occ_from = batch;
+    if constexpr (GOcc<FAM>::KKT > 1) {
+        int dev = 0, ncu = 0;
+        GHIPCHK(hipGetDevice(&dev));
+        GHIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        kkt_occ_from = 4 * ncu;
+        if (o && o->verbose) fprintf(stderr, "[mf gipm] k_gkkt occupancy variant above %d running horizons\n", kkt_occ_from);
+    }
     for (long it = 0; it < max_launches && active > 0; it += chunk) {
         const bool spec = spec_ok && active <= GSPEC_MAX;
         As.spec_of = spec ? A.spec_of : nullptr;
@@ -2695,7 +2714,10 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
                 hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch);
                 hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * GSPEC_MAX), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             }
-            hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
+            if (GOcc<FAM>::KKT > 1 && active > kkt_occ_from)
+                hipLaunchKernelGGL((k_gkkt<FAM, GOcc<FAM>::KKT>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
+            else
+                hipLaunchKernelGGL((k_gkkt<FAM, 1>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
             if (P.filter) hipLaunchKernelGGL((k_gls<FAM, true>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             else hipLaunchKernelGGL((k_gls<FAM, false>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
         }

@@ -1,7 +1,7 @@
 """Diagnostic: per-phase cycle shares of the generic solver's k_giter (build with -DMF_GSTAMPS:
 mpc_fatigue_amd/libmpcfatigue_gstamps.so, `make -C mpc_fatigue_amd libmpcfatigue_gstamps.so`).
 
-Usage: python tools/gdiag_stamps.py [batch] [iters] [case] [mode]    case: c3 (shared budget, pos_toll 1) | c4;
+Usage: python tools/gdiag_stamps.py [batch] [iters] [case] [mode]    case: c3 (shared budget, pos_toll 1) | c4 | c2 (chain);
 mode: merit (default) | ipopt (x0 = 0, filter globalisation, the reference problem at pos_toll 1e-4)
 Slots: 0 opt-error+mu, 1 barrier/residuals, 2 factor rest, 8 stage loads, 9 H assembly, 10 PB / PA,
 11 stage block, 12 BK factor, 13 BK solve + stores, 14 P update; direction (both calls): 19 stage loads,
@@ -32,6 +32,12 @@ if case == "c3":
     sp = PR.box_shared_fatigue(N=100, q0=g1)
     X = np.hstack([g1[None] + rng.uniform(-0.01, 0.01, (B, 12)), np.tile(sp["T0"], (B, 1))])
     spec, kw = dict(sp, pos_toll=1.0), dict(u_init=PR.box_u_init(sp), max_soc=4)
+elif case == "c2":  # the chain family (C2 instance of the C5 batch, merit globalisation from the line IK start)
+    from mpc_fatigue_amd import pin
+    spec = PR.pilz6_bench(N=100)
+    X = PR.pilz6_batch_q0(B, seed=0)
+    LR = pin.generate_forward_kin(PR.read_urdf(spec["urdf"]), spec["frame"]).batch(X)[0][:, :2]
+    kw = dict(max_soc=4, line_ref=np.ascontiguousarray(LR))
 else:
     spec = PR.centauro(N=50, T=2.0)
     q0 = np.asarray(spec["q0"])
