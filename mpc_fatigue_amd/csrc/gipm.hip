@@ -1159,26 +1159,60 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 for (int e = lane; e < NV * NV; e += 64) Hs[e] = (e / NV == e % NV) ? 1.0 : 0.0;
             gsync();
             GSTAMP(8);
-            // H = W + J_I^T D J_I (+ diagonal terms), in place over W (each lane its own tile)
-            tile_gemm<NV, NV, (NI > 0 ? NI : 1)>(
-                lane, [&](int a, int c) { return Hs[a * NV + c]; },
-                [&](int q, int a) { return NI > 0 ? JIs[q * NV + a] * Dds[q] : 0.0; },
-                [&](int q, int c) { return NI > 0 ? JIs[q * NV + c] : 0.0; },
-                [&](int a, int c, double v) {
-                    const bool fa = a < NX ? (k == 0) : fixs[a - NX];
-                    const bool fc = c < NX ? (k == 0) : fixs[c - NX];
-                    if (fa || fc) {
-                        v = (a == c) ? 1.0 : 0.0;
-                    } else if (a == c) {
-                        v += dw;
-                        if (a < NX) v += Vs[V_SX + a];
-                        else {
-                            v += Vs[V_SU + a - NX];
-                            if (a - NX >= P.tier1_from && a - NX < P.tier1_to) v += d1;
+            // H = W + J_I^T D J_I (+ diagonal terms), in place over W (each lane its own tile).  Small stages: the
+            // fixed rows / columns and the diagonal terms in the tile epilogue; large ones (box, Centauro: a 6 x 6
+            // tile per lane, whose unrolled per-entry tests cost more than the products) in a pass over the NV
+            // indices after it -- lane a sets row and column a of a fixed index to the identity (entries shared by
+            // two fixed lanes get the same 0) or adds + dw, + Sigma, (+ d1) to a free diagonal, in that order
+            if constexpr (NV < 24) {
+                tile_gemm<NV, NV, (NI > 0 ? NI : 1)>(
+                    lane, [&](int a, int c) { return Hs[a * NV + c]; },
+                    [&](int q, int a) { return NI > 0 ? JIs[q * NV + a] * Dds[q] : 0.0; },
+                    [&](int q, int c) { return NI > 0 ? JIs[q * NV + c] : 0.0; },
+                    [&](int a, int c, double v) {
+                        const bool fa = a < NX ? (k == 0) : fixs[a - NX];
+                        const bool fc = c < NX ? (k == 0) : fixs[c - NX];
+                        if (fa || fc) {
+                            v = (a == c) ? 1.0 : 0.0;
+                        } else if (a == c) {
+                            v += dw;
+                            if (a < NX) v += Vs[V_SX + a];
+                            else {
+                                v += Vs[V_SU + a - NX];
+                                if (a - NX >= P.tier1_from && a - NX < P.tier1_to) v += d1;
+                            }
                         }
+                        Hs[a * NV + c] = v;
+                    });
+            } else {
+                tile_gemm<NV, NV, (NI > 0 ? NI : 1)>(
+                    lane, [&](int a, int c) { return Hs[a * NV + c]; },
+                    [&](int q, int a) { return NI > 0 ? JIs[q * NV + a] * Dds[q] : 0.0; },
+                    [&](int q, int c) { return NI > 0 ? JIs[q * NV + c] : 0.0; },
+                    [&](int a, int c, double v) { Hs[a * NV + c] = v; });
+                wave_lds_sync();
+                auto hdiag = [&](int a, double v) __attribute__((always_inline)) {
+                    v += dw;
+                    if (a < NX) v += Vs[V_SX + a];
+                    else {
+                        v += Vs[V_SU + a - NX];
+                        if (a - NX >= P.tier1_from && a - NX < P.tier1_to) v += d1;
                     }
-                    Hs[a * NV + c] = v;
-                });
+                    return v;
+                };
+                auto hfixed = [&](int a) __attribute__((always_inline)) { return a < NX ? (k == 0) : (fixs[a - NX] != 0); };
+                for (int a = lane; a < NV; a += 64) {
+                    if (hfixed(a)) {
+                        for (int c = 0; c < NV; c++) {
+                            const double e = (a == c) ? 1.0 : 0.0;
+                            Hs[a * NV + c] = e;
+                            Hs[c * NV + a] = e;
+                        }
+                    } else {
+                        Hs[a * NV + a] = hdiag(a, Hs[a * NV + a]);
+                    }
+                }
+            }
             GSTAMP(9);
             tile_gemm<NX, NU, NX>(
                 lane, [](int, int) { return 0.0; }, [&](int l, int i) { return Ps[i * NX + l]; },
