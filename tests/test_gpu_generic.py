@@ -556,6 +556,27 @@ def test_concurrent_inertia_tries_equal_sequential_search(case):
     np.testing.assert_array_equal(r2.w, r1.w)
 
 
+def test_chain_occupancy_variant_equals_default():
+    """The chain families' k_gkkt has a register-capped variant (csrc/gipm.hip GOcc: 128 VGPRs, 4 waves per SIMD) that
+    the host launches while more than four horizons per CU run.  Register allocation does not change the arithmetic:
+    the first 16 horizons of a 2048-start C2 batch (IPOPT mode, every launch above the threshold on a 256-CU device)
+    end bit-identical to the same 16 solved alone (default variant)."""
+    from oracle import pin_np as P
+    from oracle.urdf_np import load_urdf_file
+    spec = PR.pilz6_bench(N=100)
+    ref = load_urdf_file(PR.urdf_path(spec["urdf"]))
+    X = np.ascontiguousarray(PR.pilz6_batch_q0(2048, seed=0))
+    lr = np.ascontiguousarray(np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in X]))
+    g = GOCP(spec)
+    kw = dict(IPOPT_MODE, max_iter=40, inertia_spec=-1)
+    rb = g.solve(x0=X, line_ref=lr, **kw)
+    rs = g.solve(x0=X[:16], line_ref=lr[:16], **kw)
+    print("2048-start batch: status", np.unique(rb.status, return_counts=True), "| first 16 iterations", rs.iters.tolist())
+    np.testing.assert_array_equal(rb.status[:16], rs.status)
+    np.testing.assert_array_equal(rb.iters[:16], rs.iters)
+    np.testing.assert_array_equal(rb.w[:16], rs.w)
+
+
 def test_watchdog_stop_with_failed_search():
     """A failed backtracking search after StopWatchDog (IPOPT's watchdog: the stored point and direction restored, the
     search from alpha_max / 2 fails): the oracle re-evaluates the stored point before it augments the filter and
