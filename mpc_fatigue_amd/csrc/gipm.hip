@@ -20,6 +20,7 @@
 #define MF_GENERIC_MODEL_PTR 1
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -68,11 +69,13 @@ enum { GP_NONE = 0, GP_SOFT = 1, GP_RESTO = 2, GP_LSM = 3, GP_IDLE = 4, GP_IDLE_
 constexpr int GFCAP = 512;  // filter entries per filter (dominated entries are dropped as IPOPT does)
 // Concurrent inertia tries: IPOPT's inertia correction is a sequential search over delta_w (0, then last / 3 or 1e-4,
 // then x8 / x100 ...), one whole Riccati factorisation per try (2.3-2.5 per iteration on C3 / C4).  When at most
-// GSPEC_MAX horizons are running -- the tail, where each horizon's serial factorisations set the batch time and the
-// device is otherwise idle -- k_gspec factors the first GNSPEC candidates of that sequence at once, one wavefront
+// GArrays::spec_max horizons are running -- the tail, where each horizon's serial factorisations set the batch time and
+// the device is otherwise idle -- k_gspec factors the first GNSPEC candidates of that sequence at once, one wavefront
 // each, into storage of their own; k_gkkt then replays the sequential search and takes a try's result (and copies its
-// factors) wherever the parameters match exactly, so the outcome is the sequential one bit for bit.
-constexpr int GNSPEC = 4, GSPEC_MAX = 64;
+// factors) wherever the parameters match exactly, so the outcome is the sequential one bit for bit.  spec_max: the
+// running count whose GNSPEC tries all fit on the device at once (k_gspec's LDS and registers; gensure_ws), at least
+// GSPEC_MIN and at most GSPEC_MAX.
+constexpr int GNSPEC = 4, GSPEC_MIN = 64, GSPEC_MAX = 1024;
 // diagnostic trace of horizon 0 in IPOPT mode (mf_gopts.verbose >= 2; mf_gdebug_trace): per iteration one row
 // from k_gpre (E_0 pieces, the restoration exit test) and one from k_gls (line search)
 constexpr int GDBG_ROWS = 4096, GDBG_W = 16;
@@ -95,6 +98,7 @@ struct GArrays {
     // storage for try t of the s-th running horizon (slist[s]; spec_of[b] = s or -1), its result code and (dw, dc)
     double *Psp, *Ksp, *Fsp, *LUsp, *Jtsp, *sdw, *sdc;
     int *slist, *spec_of, *sres;
+    int spec_max;
     const double *u_lo, *u_hi, *c_lo, *c_hi;  // shared, N x NU / N x NI
     double *x0, *lref;                        // per problem: NX, FAM::LREF (line reference / pose targets)
     const double *u0, *w0;                    // optional per-problem fixed u_0 values / warm start
@@ -502,7 +506,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     constexpr int NK = NU + NET, LDK = NK + 1;
     const int lane = threadIdx.x;
     // PH 3 (k_gspec): block s GNSPEC + t is try t of the s-th running horizon, with factor storage row blockIdx.x
-    const int b = PH == 3 ? (blockIdx.x < GNSPEC * GSPEC_MAX ? A.slist[blockIdx.x / GNSPEC] : -1) : (int)blockIdx.x;
+    const int b = PH == 3 ? (blockIdx.x < GNSPEC * A.spec_max ? A.slist[blockIdx.x / GNSPEC] : -1) : (int)blockIdx.x;
     if (b < 0 || b >= batch) return;
     GState st = A.st[b];
     if (st.status != GS_RUNNING) {
@@ -2362,7 +2366,7 @@ __global__ __launch_bounds__(64) void k_gspec(const DevModel *M0, const DevModel
                                               const DevFrame *F1, GParams P, GArrays A, int batch) {
     giter_phase<FAM, 3, true>(M0, M1, F0, F1, P, A, batch);
 }
-// the running horizons (at most GSPEC_MAX, the host's condition for launching k_gspec) listed for k_gspec
+// the running horizons (at most A.spec_max, the host's condition for launching k_gspec) listed for k_gspec
 __global__ __launch_bounds__(1024) void k_gspec_list(GArrays A, int batch) {
     __shared__ int cnt;
     if (threadIdx.x == 0) cnt = 0;
@@ -2371,13 +2375,13 @@ __global__ __launch_bounds__(1024) void k_gspec_list(GArrays A, int batch) {
         int s = -1;
         if (A.st[b].status == GS_RUNNING) {
             s = atomicAdd(&cnt, 1);
-            if (s >= GSPEC_MAX) s = -1;
+            if (s >= A.spec_max) s = -1;
             else A.slist[s] = b;
         }
         A.spec_of[b] = s;
     }
     __syncthreads();
-    for (int s = cnt + threadIdx.x; s < GSPEC_MAX; s += blockDim.x) A.slist[s] = -1;
+    for (int s = cnt + threadIdx.x; s < A.spec_max; s += blockDim.x) A.slist[s] = -1;
 }
 template <class FAM, bool FLT>
 __global__ __launch_bounds__(64) void k_gls(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
@@ -2592,15 +2596,27 @@ template <class FAM> static int gensure_ws(mf_gproblem *p, int batch, hipStream_
     GHIPCHK(hipMalloc(&p->d_st, sizeof(GState) * (size_t)batch));
     GHIPCHK(hipMalloc(&p->d_active, sizeof(int)));
     GHIPCHK(hipMalloc(&p->d_slots, sizeof(int) * (2 * (size_t)batch + 1)));
-    {  // concurrent inertia tries: GNSPEC x GSPEC_MAX factor-storage rows (k_gspec)
+    {  // concurrent inertia tries: GNSPEC x spec_max factor-storage rows (k_gspec)
         using D = typename FAM::D;
         const GSz<D> Z(p->spec.N);
-        const size_t R = (size_t)GNSPEC * GSPEC_MAX;
+        // k_gspec waves resident per CU: LDS, and the architectural VGPRs (512 per SIMD lane; a kernel that also
+        // uses accumulation registers is LDS-limited below that anyway)
+        hipFuncAttributes fa{};
+        int dev = 0, ncu = 0, lds_cu = 0;
+        GHIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k_gspec<FAM>)));
+        GHIPCHK(hipGetDevice(&dev));
+        GHIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        GHIPCHK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+        const int w_lds = fa.sharedSizeBytes > 0 ? lds_cu / (int)fa.sharedSizeBytes : 32;
+        const int w_reg = 4 * (512 / std::max(8, (fa.numRegs + 7) / 8 * 8));
+        A.spec_max = std::min(GSPEC_MAX, std::max(GSPEC_MIN, ncu * std::min(w_lds, w_reg) / GNSPEC));
+        const size_t R = (size_t)GNSPEC * A.spec_max;
         std::pair<void **, size_t> sp[] = {{(void **)&A.Psp, R * Z.P() * 8},   {(void **)&A.Ksp, R * Z.Kinv() * 8},
                                            {(void **)&A.Fsp, R * Z.Kfb() * 8}, {(void **)&A.LUsp, R * Z.lu() * 8},
                                            {(void **)&A.Jtsp, R * Z.jt() * 8}, {(void **)&A.sdw, R * 8},
                                            {(void **)&A.sdc, R * 8},           {(void **)&A.sres, R * 4},
-                                           {(void **)&A.slist, GSPEC_MAX * 4}, {(void **)&A.spec_of, (size_t)batch * 4}};
+                                           {(void **)&A.slist, (size_t)A.spec_max * 4},
+                                           {(void **)&A.spec_of, (size_t)batch * 4}};
         for (auto &it : sp) {
             void *ptr = nullptr;
             hipError_t he = hipMalloc(&ptr, it.second);
@@ -2726,6 +2742,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     const long max_launches = (2L * P.max_iter + 64) * (stream_mode ? (total + batch - 1) / batch + 1 : 1);
     // concurrent inertia tries while few horizons run (IPOPT mode; mf_gopts.inertia_spec < 0: never)
     const bool spec_ok = P.filter && !(o && o->inertia_spec < 0);
+    if (o && o->verbose && spec_ok) fprintf(stderr, "[mf gipm] concurrent inertia tries from %d running horizons\n", A.spec_max);
     GArrays As = A;  // k_gkkt's view: spec_of set while k_gspec runs
     // the occupancy variant while more than four horizons per CU run (measured crossover on the C2 leg: launches
     // at ~1000 running horizons take the same time with either variant, fewer run faster without spills)
@@ -2738,7 +2755,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
         if (o && o->verbose) fprintf(stderr, "[mf gipm] k_gkkt occupancy variant above %d running horizons\n", kkt_occ_from);
     }
     for (long it = 0; it < max_launches && active > 0; it += chunk) {
-        const bool spec = spec_ok && active <= GSPEC_MAX;
+        const bool spec = spec_ok && active <= A.spec_max;
         As.spec_of = spec ? A.spec_of : nullptr;
         for (int c = 0; c < chunk; c++) {
             hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
@@ -2746,7 +2763,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             hipLaunchKernelGGL(k_gpre<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             if (spec) {
                 hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch);
-                hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * GSPEC_MAX), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+                hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * A.spec_max), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             }
             if (GOcc<FAM>::KKT > 1 && active > kkt_occ_from)
                 hipLaunchKernelGGL((k_gkkt<FAM, GOcc<FAM>::KKT>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
