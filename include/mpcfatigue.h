@@ -236,8 +236,10 @@ typedef struct {
     double bound_relax;    /* IPOPT bound_relax_factor (1e-8 in IPOPT; 0 = exact bounds) */
     int resto_hard_dyn;    /* 1: the restoration problem keeps x_{k+1} = f(x_k, u_k) exact (no elastic variables on
                               the dynamics rows; the build's variant before round 5); 0: IPOPT's restoration */
-    int inertia_spec;      /* IPOPT mode: while at most 64 horizons run, the first 4 inertia-correction tries of each
-                              iteration are factored concurrently (same result as the sequential search); -1: never */
+    int inertia_spec;      /* IPOPT mode: while few horizons run (at most as many as can hold 4 tries each on the
+                              device at once: C3 192, C4 128, chain 512 on MI355X, at least 64), the first 4
+                              inertia-correction tries of each iteration are factored concurrently (same result as
+                              the sequential search); -1: never */
 } mf_gopts;
 
 int mf_gproblem_create(const mf_model *m0, const mf_model *m1, const mf_gspec *spec, mf_gproblem **out);
