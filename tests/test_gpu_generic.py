@@ -480,6 +480,41 @@ def test_c2_ipopt_mode_matches_oracle():
         assert np.abs(g.q_traj(r.w[b]) - g.q_traj(W[b])).max() < 1e-6
 
 
+def test_c2_ipopt_mode_sixteen_horizons_match_oracle():
+    """The bench's C2 leg as the reference solves it (IPOPT mode from x0 = 0, the generic solver's chain family) on 16
+    horizons spread over the 4096-start draw (every 256th) against the oracle's IPOPT-mode solves with the device's
+    elimination (riccati = 2): the same status everywhere; where the iteration paths agree (same iteration count)
+    the same solution (q 1e-6 rad, objective 1e-8); where they part at round-off inside a restoration phase, a
+    neighbouring optimum of C2's flat valley (objective 1e-4, iterations within 10 %, q 0.05 rad)."""
+    from oracle import pin_np as P
+    from oracle.urdf_np import load_urdf_file
+    N = 100
+    base = PR.pilz6_bench(N=N)
+    ref = load_urdf_file(PR.urdf_path(base["urdf"]))
+    idx = np.arange(0, 4096, 256)
+    Q0 = PR.pilz6_batch_q0(4096, seed=0)[idx]
+    LR = np.array([P.forward_kinematics(ref, q, "prbt_link_5")[0][:2] for q in Q0])
+    kw = dict(IPOPT_MODE, max_iter=3000)
+    g = GOCP(base)
+    r = g.solve(x0=Q0, line_ref=LR, **kw)
+    specs = [PR.pilz6_bench(N=N, q0=Q0[b], line_ref=LR[b]) for b in range(len(idx))]
+    W, R = G.solve_batch(specs, nthreads=8, riccati=2, **kw)
+    same = 0
+    for b in range(len(idx)):
+        dq = np.abs(g.q_traj(r.w[b]) - g.q_traj(W[b])).max()
+        dobj = abs(float(r.obj[b]) - R[b].obj) / abs(R[b].obj)
+        print(f"start {idx[b]}: device {int(r.status[b])}/{int(r.iters[b])} it, oracle {R[b].status}/{R[b].iter} it, "
+              f"dq {dq:.2e}, dobj {dobj:.1e}")
+        assert int(r.status[b]) == R[b].status == 0, (idx[b], int(r.status[b]), R[b].status)
+        if int(r.iters[b]) == R[b].iter:
+            same += 1
+            assert dq < 1e-6 and dobj < 1e-8, (idx[b], dq, dobj)
+        else:
+            assert dobj < 1e-4 and abs(int(r.iters[b]) - R[b].iter) <= 0.1 * R[b].iter and dq < 0.05, \
+                (idx[b], int(r.iters[b]), R[b].iter, dq, dobj)
+    print("identical paths:", same, "of", len(idx))
+
+
 def test_c2_ipopt_restoration_with_elastic_dynamics_rows():
     """IPOPT's restoration problem (IpRestoIpoptNLP: elastic p, n on every constraint row, the dynamics rows
     x_{k+1} = f(x_k, u_k) included) on the device: the Riccati recursion through the relaxed rows
