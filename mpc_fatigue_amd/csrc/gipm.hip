@@ -2342,23 +2342,32 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     }
 }
 
-// k_gkkt's occupancy variant for full launches.  The chain families' stage arrays take ~6 KB of LDS, so their
-// k_gkkt is register-limited: at the default allocation (152 VGPRs) a CU holds 12 horizons and a 4096-horizon
-// launch runs in two rounds of waves that are latency-bound (lone and fully loaded waves take nearly the same
-// cycles per stage).  Capped at 128 VGPRs (4 waves per SIMD, some spills) the whole launch is resident: the
-// host takes this variant while many horizons run, the default one (no spills, faster lone waves) in the tail.  The box and Centauro families are LDS-limited (~50 KB: three
-// horizons per CU) and have only the default.
-template <class FAM> struct GOcc { static constexpr int KKT = 1; };
-template <int NJ, int NF, int NE, bool TH> struct GOcc<ChainFam<NJ, NF, NE, TH>> { static constexpr int KKT = 4; };
+// Occupancy variants of k_gkkt / k_gls for full launches.  The chain families' stage arrays take ~6 KB of LDS, so
+// these kernels are register-limited: the compiler's own allocation (k_gkkt 256 + 40 accumulation registers, k_gls
+// about 430) leaves one wave per SIMD, four horizons per CU, and a 4096-horizon launch runs in four rounds of waves
+// that are latency-bound (lone and fully loaded waves take nearly the same cycles per stage).  k_gkkt capped at 128
+// registers (4 waves per SIMD, 253 spilled) and k_gls at 256 (2 waves, 208 spilled) hold 4x / 2x the horizons: the host takes them while more horizons run than the default kernels hold (four per CU),
+// the defaults (no spills, faster lone waves) in the tail.  The box and Centauro families are LDS-limited (~50 KB:
+// three horizons per CU) and have only the defaults.
+template <class FAM> struct GOcc { static constexpr int KKT = 1, LS = 1; };
+template <int NJ, int NF, int NE, bool TH> struct GOcc<ChainFam<NJ, NF, NE, TH>> {
+    static constexpr int KKT = 4, LS = 2;
+};
 
 template <class FAM>
 __global__ __launch_bounds__(64) void k_gpre(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
     giter_phase<FAM, 0, true>(M0, M1, F0, F1, P, A, batch);
 }
-template <class FAM, int OCC>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_gkkt(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
+template <class FAM>
+__global__ __launch_bounds__(64) void k_gkkt(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                              const DevFrame *F1, GParams P, GArrays A, int batch) {
+    giter_phase<FAM, 1, true>(M0, M1, F0, F1, P, A, batch);
+}
+// the register-capped variant (GOcc): its own kernel, so the default one keeps the compiler's own allocation
+template <class FAM, int OCC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_gkkt_occ(
+    const DevModel *M0, const DevModel *M1, const DevFrame *F0, const DevFrame *F1, GParams P, GArrays A, int batch) {
     giter_phase<FAM, 1, true>(M0, M1, F0, F1, P, A, batch);
 }
 template <class FAM>
@@ -2386,6 +2395,11 @@ __global__ __launch_bounds__(1024) void k_gspec_list(GArrays A, int batch) {
 template <class FAM, bool FLT>
 __global__ __launch_bounds__(64) void k_gls(const DevModel *M0, const DevModel *M1, const DevFrame *F0,
                                             const DevFrame *F1, GParams P, GArrays A, int batch) {
+    giter_phase<FAM, 2, FLT>(M0, M1, F0, F1, P, A, batch);
+}
+template <class FAM, bool FLT, int OCC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void k_gls_occ(
+    const DevModel *M0, const DevModel *M1, const DevFrame *F0, const DevFrame *F1, GParams P, GArrays A, int batch) {
     giter_phase<FAM, 2, FLT>(M0, M1, F0, F1, P, A, batch);
 }
 
@@ -2744,8 +2758,8 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     const bool spec_ok = P.filter && !(o && o->inertia_spec < 0);
     if (o && o->verbose && spec_ok) fprintf(stderr, "[mf gipm] concurrent inertia tries from %d running horizons\n", A.spec_max);
     GArrays As = A;  // k_gkkt's view: spec_of set while k_gspec runs
-    // the occupancy variant while more than four horizons per CU run (measured crossover on the C2 leg: launches
-    // at ~1000 running horizons take the same time with either variant, fewer run faster without spills)
+    // the occupancy variants while more horizons run than the default kernels hold (four per CU; measured on the C2
+    // leg: launches at ~1000 running horizons take the same time with either k_gkkt, fewer run faster without spills)
     int kkt_occ_from = batch;
     if constexpr (GOcc<FAM>::KKT > 1) {
         int dev = 0, ncu = 0;
@@ -2765,12 +2779,28 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
                 hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch);
                 hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * A.spec_max), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             }
-            if (GOcc<FAM>::KKT > 1 && active > kkt_occ_from)
-                hipLaunchKernelGGL((k_gkkt<FAM, GOcc<FAM>::KKT>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
-            else
-                hipLaunchKernelGGL((k_gkkt<FAM, 1>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
-            if (P.filter) hipLaunchKernelGGL((k_gls<FAM, true>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
-            else hipLaunchKernelGGL((k_gls<FAM, false>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            bool occ = false;
+            if constexpr (GOcc<FAM>::KKT > 1) {
+                occ = active > kkt_occ_from;
+                if (occ)
+                    hipLaunchKernelGGL((k_gkkt_occ<FAM, GOcc<FAM>::KKT>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P,
+                                       As, batch);
+            }
+            if (!occ) hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
+            bool occ_ls = false;
+            if constexpr (GOcc<FAM>::LS > 1) {
+                occ_ls = active > kkt_occ_from;
+                if (occ_ls && P.filter)
+                    hipLaunchKernelGGL((k_gls_occ<FAM, true, GOcc<FAM>::LS>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1,
+                                       P, A, batch);
+                else if (occ_ls)
+                    hipLaunchKernelGGL((k_gls_occ<FAM, false, GOcc<FAM>::LS>), dim3(batch), dim3(64), 0, s, M0, M1, F0,
+                                       F1, P, A, batch);
+            }
+            if (!occ_ls && P.filter)
+                hipLaunchKernelGGL((k_gls<FAM, true>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            else if (!occ_ls)
+                hipLaunchKernelGGL((k_gls<FAM, false>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
         }
         GHIPCHK(hipGetLastError());
         GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
