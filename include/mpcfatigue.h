@@ -242,6 +242,10 @@ typedef struct {
                               the sequential search); -1: never */
 } mf_gopts;
 
+/* Fills *o with the library's defaults (tol = constr_viol_tol = 1e-8, max_iter 3000, mu_init 0.1, max_soc 4, every
+ * other field 0 / NULL) and returns sizeof(mf_gopts).  C callers start from it and set what they need, so fields a
+ * later version appends start at their defaults (the struct has no size field). */
+int mf_gopts_init(mf_gopts *o);
 int mf_gproblem_create(const mf_model *m0, const mf_model *m1, const mf_gspec *spec, mf_gproblem **out);
 void mf_gproblem_free(mf_gproblem *p);
 /* dims = {nx, nu, ni, ne, wsize} */
@@ -271,6 +275,15 @@ int mf_gnode_record(mf_gproblem *p, const double *xu, const double *yi, const do
 /* Diagnostics: dual state of problem b after the last solve, [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU |
  * mu] (per-node blocks as the solver stores them).  Returns the number of doubles written. */
 int mf_gdebug_duals(mf_gproblem *p, int b, double *out);
+/* Diagnostics: the slack rows s (N x ni, node-major) of problem b after the last solve -- with mf_gdebug_duals the
+ * primal-dual point an oracle-side KKT check of a device solution needs.  Returns N x ni. */
+int mf_gdebug_slacks(mf_gproblem *p, int b, double *out);
+/* Per-phase timing of the generic solver (HIP events on the solve stream around every launch group; bench.py):
+ * enable != 0 turns it on and resets the accumulators.  kernel_stats: total ms and launches per slot
+ * {k_geval, k_gasm, k_gpre, k_gkkt (with k_gspec and the occupancy variant), k_gls}, and (node_evals, may be
+ * NULL) the node evaluations k_geval made while timing was on. */
+int mf_gproblem_timing(mf_gproblem *p, int enable);
+int mf_gproblem_kernel_stats(mf_gproblem *p, double *ms5, long *launches5, long long *node_evals);
 /* Diagnostics: solver counters of problem b after the last solve, out[10] = {iterations, status, inertia corrections,
  * line-search failures, second-order-correction steps, restoration phases, watchdog starts, soft-restoration steps,
  * failed searches after StopWatchDog, restoration-phase iterations}.  Returns 10. */

@@ -86,13 +86,44 @@ class SolverOpts(C.Structure):
 _lib = None
 
 
+def _hip_runtimes() -> list[str]:
+    """Distinct libamdhip64 files mapped into this process (/proc/self/maps)."""
+    seen = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.strip() else ""
+                if "libamdhip64" in os.path.basename(p):
+                    seen.add(os.path.realpath(p))
+    except OSError:
+        pass
+    return sorted(seen)
+
+
+def _torch_runtime_first() -> None:
+    """One HIP runtime per process.  torch bundles its own libamdhip64 under the same soname (libamdhip64.so.7) as
+    the ROCm one this library links; its libc10_hip asks for it by the unversioned name, so if ROCm's copy were
+    mapped first torch would map a second runtime next to it and report "No HIP GPUs are available".  Importing
+    torch first (when it is installed) maps torch's runtime, and the dynamic linker then satisfies this library's
+    libamdhip64.so.7 with that same object."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MFError(-4, f"{LIB_PATH} not built (run __graft_entry__.build() or make -C mpc_fatigue_amd)")
+    _torch_runtime_first()
     L = C.CDLL(LIB_PATH)
+    rt = _hip_runtimes()
+    if len(rt) > 1:
+        raise MFError(-4, "two HIP runtimes mapped in one process (" + ", ".join(rt) + "): import torch before "
+                          "anything that loads ROCm's libamdhip64 directly")
     vp, dp, ip, cp = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int), C.c_char_p
     sig = {
         "mf_model_from_urdf": ([cp, C.POINTER(vp)], C.c_int),
@@ -122,6 +153,7 @@ def lib() -> C.CDLL:
         "mf_ik_batch": ([vp, C.c_int, dp, dp, dp, dp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double], C.c_int),
         "mf_ik_batch_dev": ([vp, C.c_int, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, vp],
                             C.c_int),
+        "mf_gopts_init": ([C.POINTER(GOpts)], C.c_int),
         "mf_gproblem_create": ([vp, vp, C.POINTER(GSpec), C.POINTER(vp)], C.c_int),
         "mf_gproblem_free": ([vp], None),
         "mf_gproblem_dims": ([vp, ip], C.c_int),
@@ -131,6 +163,9 @@ def lib() -> C.CDLL:
                                  C.c_int),
         "mf_gnode_record": ([vp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
         "mf_gdebug_duals": ([vp, C.c_int, dp], C.c_int),
+        "mf_gdebug_slacks": ([vp, C.c_int, dp], C.c_int),
+        "mf_gproblem_timing": ([vp, C.c_int], C.c_int),
+        "mf_gproblem_kernel_stats": ([vp, dp, C.POINTER(C.c_long), C.POINTER(C.c_longlong)], C.c_int),
         "mf_gdebug_counters": ([vp, C.c_int, ip], C.c_int),
         "mf_gdebug_trace": ([dp], C.c_int),
         "mf_gdebug_trace_reset": ([], C.c_int),
@@ -150,9 +185,10 @@ EXPORTED_SYMBOLS = [
     "mf_problem_wsize", "mf_node_eval", "mf_solve_batch", "mf_solve_batch_dev", "mf_solve_batch_ws",
     "mf_solve_batch_ws_dev", "mf_problem_timing",
     "mf_problem_kernel_stats", "mf_problem_trace", "mf_kernel_name", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
-    "mf_gproblem_create", "mf_gproblem_free", "mf_gproblem_dims", "mf_gsolve_batch", "mf_gsolve_batch_dev",
+    "mf_gopts_init", "mf_gproblem_create", "mf_gproblem_free", "mf_gproblem_dims", "mf_gsolve_batch", "mf_gsolve_batch_dev",
     "mf_gsolve_stream_dev",
-    "mf_gnode_record", "mf_gdebug_duals", "mf_gdebug_counters", "mf_gdebug_trace", "mf_gdebug_trace_reset",
+    "mf_gnode_record", "mf_gdebug_duals", "mf_gdebug_slacks", "mf_gproblem_timing", "mf_gproblem_kernel_stats",
+    "mf_gdebug_counters", "mf_gdebug_trace", "mf_gdebug_trace_reset",
 ]
 
 

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -116,6 +117,7 @@ struct GArrays {
     // k_ginit then initialises (init[b] = 1).  pidx == nullptr: slot b is problem b (mf_gsolve_batch*).
     int *pidx, *next, *init;
     int total;
+    unsigned long long *neval;  // timing mode (mf_gproblem_timing): node evaluations made by k_geval, else nullptr
     const double *x0all, *lrall;  // every problem's x_0 and line reference (total rows)
     double *ow, *okkt, *oobj;     // every problem's outputs
     int *ost, *oit;
@@ -343,7 +345,10 @@ __global__ __launch_bounds__(256) void k_geval(const DevModel *M0, const DevMode
     if (run && t == 0) FAM::seeds(P, u, yi, ye, lam, eqon, ow, S[g]);
     __syncthreads();
     if (run) FAM::lane(M, F, x, u, yi, t, S[g]);
-    __syncthreads();
+    {
+        const int nrun = __syncthreads_count(run && t == 0);  // (also the barrier before the scratch store)
+        if (A.neval && tid == 0 && nrun > 0) atomicAdd(A.neval, (unsigned long long)nrun);
+    }
 #ifdef MF_GSTAMPS
     const unsigned long long gs1_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -2551,7 +2556,16 @@ struct mf_gproblem {
     GState *d_st = nullptr;
     int *d_active = nullptr;
     int *d_slots = nullptr;  // continuous batching: pidx (cap) | init (cap) | next (1)
-    std::vector<void *> sbufs;  // concurrent inertia tries: storage rows, result codes, horizon lists
+    std::vector<void *> sbufs;  // per-horizon slot of the concurrent inertia tries (spec_of)
+    std::vector<void *> spec_bufs;  // their storage rows, result codes, horizon list (gensure_spec)
+    int spec_cap = 0;               // running horizons whose tries fit on the device at once (gensure_ws)
+    // per-phase timing (HIP events on the solve stream around every launch group), mf_gproblem_timing:
+    // slots k_geval, k_gasm, k_gpre, k_gkkt (with k_gspec / the occupancy variant), k_gls
+    int timing = 0;
+    unsigned long long *d_neval = nullptr;
+    std::vector<hipEvent_t> ev;
+    double t_ms[5] = {0, 0, 0, 0, 0};
+    long t_launch[5] = {0, 0, 0, 0, 0};
 };
 
 template <class FAM> static void sizes_of(int N, std::vector<std::pair<double **, size_t>> &items, GArrays &A) {
@@ -2580,6 +2594,9 @@ static void gfree_ws(mf_gproblem *p) {
     p->bufs.clear();
     for (void *b : p->sbufs) (void)hipFree(b);
     p->sbufs.clear();
+    for (void *b : p->spec_bufs) (void)hipFree(b);
+    p->spec_bufs.clear();
+    p->A.spec_max = 0;
     if (p->d_st) (void)hipFree(p->d_st);
     if (p->d_active) (void)hipFree(p->d_active);
     if (p->d_slots) (void)hipFree(p->d_slots);
@@ -2610,37 +2627,30 @@ template <class FAM> static int gensure_ws(mf_gproblem *p, int batch, hipStream_
     GHIPCHK(hipMalloc(&p->d_st, sizeof(GState) * (size_t)batch));
     GHIPCHK(hipMalloc(&p->d_active, sizeof(int)));
     GHIPCHK(hipMalloc(&p->d_slots, sizeof(int) * (2 * (size_t)batch + 1)));
-    {  // concurrent inertia tries: GNSPEC x spec_max factor-storage rows (k_gspec)
-        using D = typename FAM::D;
-        const GSz<D> Z(p->spec.N);
-        // k_gspec waves resident per CU: LDS, and the architectural VGPRs (512 per SIMD lane; a kernel that also
-        // uses accumulation registers is LDS-limited below that anyway)
+    {  // concurrent inertia tries (k_gspec): the running count whose GNSPEC tries all fit on the device at once; the
+       // factor-storage rows themselves are made on demand by gensure_spec (IPOPT mode with the tries on only)
         hipFuncAttributes fa{};
         int dev = 0, ncu = 0, lds_cu = 0;
         GHIPCHK(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(k_gspec<FAM>)));
         GHIPCHK(hipGetDevice(&dev));
         GHIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         GHIPCHK(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
+        // k_gspec waves resident per CU: LDS, and the architectural VGPRs (512 per SIMD lane; a kernel that also
+        // uses accumulation registers is LDS-limited below that anyway)
         const int w_lds = fa.sharedSizeBytes > 0 ? lds_cu / (int)fa.sharedSizeBytes : 32;
         const int w_reg = 4 * (512 / std::max(8, (fa.numRegs + 7) / 8 * 8));
-        A.spec_max = std::min(GSPEC_MAX, std::max(GSPEC_MIN, ncu * std::min(w_lds, w_reg) / GNSPEC));
-        const size_t R = (size_t)GNSPEC * A.spec_max;
-        std::pair<void **, size_t> sp[] = {{(void **)&A.Psp, R * Z.P() * 8},   {(void **)&A.Ksp, R * Z.Kinv() * 8},
-                                           {(void **)&A.Fsp, R * Z.Kfb() * 8}, {(void **)&A.LUsp, R * Z.lu() * 8},
-                                           {(void **)&A.Jtsp, R * Z.jt() * 8}, {(void **)&A.sdw, R * 8},
-                                           {(void **)&A.sdc, R * 8},           {(void **)&A.sres, R * 4},
-                                           {(void **)&A.slist, (size_t)A.spec_max * 4},
-                                           {(void **)&A.spec_of, (size_t)batch * 4}};
-        for (auto &it : sp) {
-            void *ptr = nullptr;
-            hipError_t he = hipMalloc(&ptr, it.second);
-            if (he != hipSuccess) {
-                gfree_ws(p);
-                return capi_fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
-            }
-            p->sbufs.push_back(ptr);
-            *it.first = ptr;
+        p->spec_cap = std::min(GSPEC_MAX, std::max(GSPEC_MIN, ncu * std::min(w_lds, w_reg) / GNSPEC));
+        A.spec_max = 0;
+        A.Psp = A.Ksp = A.Fsp = A.LUsp = A.Jtsp = A.sdw = A.sdc = nullptr;
+        A.sres = A.slist = nullptr;
+        void *ptr = nullptr;
+        hipError_t he = hipMalloc(&ptr, (size_t)batch * 4);
+        if (he != hipSuccess) {
+            gfree_ws(p);
+            return capi_fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
         }
+        p->sbufs.push_back(ptr);
+        A.spec_of = static_cast<int *>(ptr);
     }
     A.st = p->d_st;
     A.active = p->d_active;
@@ -2649,6 +2659,37 @@ template <class FAM> static int gensure_ws(mf_gproblem *p, int batch, hipStream_
     A.c_lo = p->d_clo;
     A.c_hi = p->d_chi;
     p->cap = batch;
+    return MF_OK;
+}
+
+// the factor-storage rows of the concurrent inertia tries for `rows` running horizons (GNSPEC tries each; made on
+// the first IPOPT-mode solve that uses them, never for merit mode or inertia_spec < 0; kept with the workspace)
+template <class FAM> static int gensure_spec(mf_gproblem *p, int rows) {
+    using D = typename FAM::D;
+    GArrays &A = p->A;
+    if (A.spec_max >= rows) return MF_OK;
+    for (void *b : p->spec_bufs) (void)hipFree(b);
+    p->spec_bufs.clear();
+    A.spec_max = 0;
+    const GSz<D> Z(p->spec.N);
+    const size_t R = (size_t)GNSPEC * rows;
+    std::pair<void **, size_t> sp[] = {{(void **)&A.Psp, R * Z.P() * 8},   {(void **)&A.Ksp, R * Z.Kinv() * 8},
+                                       {(void **)&A.Fsp, R * Z.Kfb() * 8}, {(void **)&A.LUsp, R * Z.lu() * 8},
+                                       {(void **)&A.Jtsp, R * Z.jt() * 8}, {(void **)&A.sdw, R * 8},
+                                       {(void **)&A.sdc, R * 8},           {(void **)&A.sres, R * 4},
+                                       {(void **)&A.slist, (size_t)rows * 4}};
+    for (auto &it : sp) {
+        void *ptr = nullptr;
+        hipError_t he = hipMalloc(&ptr, it.second);
+        if (he != hipSuccess) {
+            for (void *b : p->spec_bufs) (void)hipFree(b);
+            p->spec_bufs.clear();
+            return capi_fail(MF_ERR_NOMEM, std::string("workspace allocation failed: ") + hipGetErrorString(he));
+        }
+        p->spec_bufs.push_back(ptr);
+        *it.first = ptr;
+    }
+    A.spec_max = rows;
     return MF_OK;
 }
 
@@ -2709,6 +2750,14 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     A.u_lo = ulo; A.u_hi = uhi; A.c_lo = clo; A.c_hi = chi;
     A.pidx = A.next = A.init = nullptr;
     A.total = total;
+    A.neval = nullptr;
+    if (p->timing) {
+        if (!p->d_neval) {
+            GHIPCHK(hipMalloc(&p->d_neval, sizeof(unsigned long long)));
+            GHIPCHK(hipMemsetAsync(p->d_neval, 0, sizeof(unsigned long long), s));
+        }
+        A.neval = p->d_neval;
+    }
     A.x0all = d_x0;
     A.lrall = FAM::LREF == 2 ? d_lref : nullptr;
     A.ow = d_w; A.okkt = d_kkt; A.oobj = d_obj; A.ost = d_status; A.oit = d_iters;
@@ -2753,9 +2802,19 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     // every running horizon ends at the latest when its own iteration count reaches max_iter; in IPOPT mode
     // some launches advance no iteration (the restoration phase's start and end), so the host bound is on
     // launches, with room for those, not on iterations
-    const long max_launches = (2L * P.max_iter + 64) * (stream_mode ? (total + batch - 1) / batch + 1 : 1);
+    // (IPOPT mode: a soft step undone, the restoration's start and one of its iterations take up to 5 launch rounds
+    // for 2 iterations)
+    const long max_launches = (3L * P.max_iter + 64) * (stream_mode ? (total + batch - 1) / batch + 1 : 1);
     // concurrent inertia tries while few horizons run (IPOPT mode; mf_gopts.inertia_spec < 0: never)
     const bool spec_ok = P.filter && !(o && o->inertia_spec < 0);
+    if (spec_ok) {
+        if ((e = gensure_spec<FAM>(p, std::min(p->spec_cap, batch)))) return e;
+        A.Psp = p->A.Psp; A.Ksp = p->A.Ksp; A.Fsp = p->A.Fsp; A.LUsp = p->A.LUsp; A.Jtsp = p->A.Jtsp;
+        A.sdw = p->A.sdw; A.sdc = p->A.sdc; A.sres = p->A.sres; A.slist = p->A.slist;
+        A.spec_max = std::min(p->spec_cap, batch);
+    } else {
+        A.spec_max = 0;
+    }
     if (o && o->verbose && spec_ok) fprintf(stderr, "[mf gipm] concurrent inertia tries from %d running horizons\n", A.spec_max);
     GArrays As = A;  // k_gkkt's view: spec_of set while k_gspec runs
     // the occupancy variants while more horizons run than the default kernels hold (four per CU; measured on the C2
@@ -2768,16 +2827,34 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
         kkt_occ_from = 4 * ncu;
         if (o && o->verbose) fprintf(stderr, "[mf gipm] k_gkkt occupancy variant above %d running horizons\n", kkt_occ_from);
     }
+    const auto t_start = std::chrono::steady_clock::now();
+    constexpr int NPH = 5;
+    if (p->timing && p->ev.size() < (size_t)(2 * NPH * chunk)) {
+        for (auto e2 : p->ev) (void)hipEventDestroy(e2);
+        p->ev.assign(2 * NPH * chunk, nullptr);
+        for (auto &e2 : p->ev) GHIPCHK(hipEventCreate(&e2));
+    }
+    auto mark = [&](int c, int ph, int end) {
+        if (p->timing) (void)hipEventRecord(p->ev[(c * NPH + ph) * 2 + end], s);
+    };
     for (long it = 0; it < max_launches && active > 0; it += chunk) {
         const bool spec = spec_ok && active <= A.spec_max;
         As.spec_of = spec ? A.spec_of : nullptr;
         for (int c = 0; c < chunk; c++) {
+            mark(c, 0, 0);
             hipLaunchKernelGGL(k_geval<FAM>, dim3(eval_blocks), dim3(256), 0, s, M0, M1, F0, F1, P, A, batch);
+            mark(c, 0, 1);
+            mark(c, 1, 0);
             hipLaunchKernelGGL(k_gasm<FAM>, dim3(rec_blocks), dim3(256), 0, s, P, A, batch);
+            mark(c, 1, 1);
+            mark(c, 2, 0);
             hipLaunchKernelGGL(k_gpre<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            mark(c, 2, 1);
+            mark(c, 3, 0);
             if (spec) {
                 hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch);
-                hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * A.spec_max), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+                hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * std::min(active, A.spec_max)), dim3(64), 0, s, M0, M1, F0,
+                                   F1, P, A, batch);
             }
             bool occ = false;
             if constexpr (GOcc<FAM>::KKT > 1) {
@@ -2787,6 +2864,8 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
                                        As, batch);
             }
             if (!occ) hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
+            mark(c, 3, 1);
+            mark(c, 4, 0);
             bool occ_ls = false;
             if constexpr (GOcc<FAM>::LS > 1) {
                 occ_ls = active > kkt_occ_from;
@@ -2801,10 +2880,19 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
                 hipLaunchKernelGGL((k_gls<FAM, true>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             else if (!occ_ls)
                 hipLaunchKernelGGL((k_gls<FAM, false>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
+            mark(c, 4, 1);
         }
         GHIPCHK(hipGetLastError());
         GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
         GHIPCHK(hipStreamSynchronize(s));
+        if (p->timing)
+            for (int c = 0; c < chunk; c++)
+                for (int ph = 0; ph < NPH; ph++) {
+                    float ms = 0.f;
+                    GHIPCHK(hipEventElapsedTime(&ms, p->ev[(c * NPH + ph) * 2], p->ev[(c * NPH + ph) * 2 + 1]));
+                    p->t_ms[ph] += ms;
+                    p->t_launch[ph]++;
+                }
         if (stream_mode && active < batch) {  // finished slots: outputs written, next problems handed out
             hipLaunchKernelGGL(k_gharvest<FAM>, dim3(batch), dim3(64), 0, s, A, P.N, batch, 0);
             hipLaunchKernelGGL(k_ginit<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
@@ -2812,7 +2900,9 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             GHIPCHK(hipMemcpyAsync(&active, A.active, sizeof(int), hipMemcpyDeviceToHost, s));
             GHIPCHK(hipStreamSynchronize(s));
         }
-        if (o && o->verbose) fprintf(stderr, "[mf gipm] after %ld launches: %d running\n", it + chunk, active);
+        if (o && o->verbose)
+            fprintf(stderr, "[mf gipm] after %ld launches: %d running, %.3f ms\n", it + chunk, active,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
     }
     if (stream_mode) {  // launch bound reached with slots still running: written out as max_iter
         hipLaunchKernelGGL(k_gharvest<FAM>, dim3(batch), dim3(64), 0, s, A, P.N, batch, 1);
@@ -2841,6 +2931,19 @@ static int gdispatch_solve(mf_gproblem *p, int batch, const double *x0, const do
 
 template <class FAM> static void dims_of(int &nx, int &nu, int &ni, int &ne) {
     nx = FAM::D::NX; nu = FAM::D::NU; ni = FAM::D::NI; ne = FAM::D::NE;
+}
+
+// mf_gopts with the library's defaults (include/mpcfatigue.h): callers fill this and change what they need, so a
+// field added in a later version starts at its default instead of at whatever a shorter struct leaves behind
+extern "C" int mf_gopts_init(mf_gopts *o) {
+    if (!o) return capi_fail(MF_ERR_ARG, "null argument");
+    memset(o, 0, sizeof *o);
+    o->tol = 1e-8;
+    o->constr_viol_tol = 1e-8;
+    o->max_iter = 3000;
+    o->mu_init = 0.1;
+    o->max_soc = 4;
+    return (int)sizeof *o;
 }
 
 extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, const mf_gspec *spec, mf_gproblem **out) {
@@ -2949,9 +3052,35 @@ extern "C" int mf_gproblem_create(const mf_model *m0c, const mf_model *m1c, cons
 extern "C" void mf_gproblem_free(mf_gproblem *p) {
     if (!p) return;
     gfree_ws(p);
+    for (auto e : p->ev) (void)hipEventDestroy(e);
+    if (p->d_neval) (void)hipFree(p->d_neval);
     for (double *d : {p->d_ulo, p->d_uhi, p->d_clo, p->d_chi, p->d_ulo_r, p->d_uhi_r, p->d_clo_r, p->d_chi_r})
         if (d) (void)hipFree(d);
     delete p;
+}
+
+// per-phase timing of the generic solver's launches (HIP events on the solve stream; diagnostics and bench.py):
+// enable resets the accumulators; stats: total ms and launch count per slot
+// {k_geval, k_gasm, k_gpre, k_gkkt (+ k_gspec, occupancy variant), k_gls}
+extern "C" int mf_gproblem_timing(mf_gproblem *p, int enable) {
+    if (!p) return capi_fail(MF_ERR_ARG, "null argument");
+    p->timing = enable ? 1 : 0;
+    for (int k = 0; k < 5; k++) { p->t_ms[k] = 0; p->t_launch[k] = 0; }
+    if (p->d_neval) GHIPCHK(hipMemset(p->d_neval, 0, sizeof(unsigned long long)));
+    return MF_OK;
+}
+extern "C" int mf_gproblem_kernel_stats(mf_gproblem *p, double *ms5, long *launches5, long long *node_evals) {
+    if (!p || !ms5 || !launches5) return capi_fail(MF_ERR_ARG, "null argument");
+    for (int k = 0; k < 5; k++) { ms5[k] = p->t_ms[k]; launches5[k] = p->t_launch[k]; }
+    if (node_evals) {
+        unsigned long long v = 0;
+        if (p->d_neval) {
+            GHIPCHK(hipDeviceSynchronize());
+            GHIPCHK(hipMemcpy(&v, p->d_neval, sizeof v, hipMemcpyDeviceToHost));
+        }
+        *node_evals = (long long)v;
+    }
+    return MF_OK;
 }
 
 extern "C" int mf_gproblem_dims(const mf_gproblem *p, int *dims5) {
@@ -3166,6 +3295,34 @@ extern "C" int mf_gdebug_counters(mf_gproblem *p, int b, int *out) {
                        st.n_wdfail, st.n_rit};
     for (int i = 0; i < 10; i++) out[i] = v[i];
     return 10;
+}
+
+// diagnostics: the slack rows s (N x NI) of problem b after the last solve (with mf_gdebug_duals, the primal-dual
+// point an oracle-side KKT check of the device's solution needs)
+template <class FAM> static int gslack_core(mf_gproblem *p, int b, double *out) {
+    using D = typename FAM::D;
+    const GSz<D> Z(p->spec.N);
+    if (b < 0 || b >= p->last_batch) return capi_fail(MF_ERR_ARG, "problem index out of range (last solve's batch)");
+    GHIPCHK(hipDeviceSynchronize());
+    std::vector<double> s(Z.i());
+    GHIPCHK(hipMemcpy(s.data(), p->A.s + (size_t)b * Z.i(), Z.i() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int k = 0; k < p->spec.N; k++)
+        for (int q = 0; q < D::NI; q++) out[(size_t)k * D::NI + q] = s[(size_t)k * D::NIA + q];
+    return p->spec.N * D::NI;
+}
+
+extern "C" int mf_gdebug_slacks(mf_gproblem *p, int b, double *out) {
+    if (!p || !out) return capi_fail(MF_ERR_ARG, "null argument");
+    switch (p->kind) {
+        case GK_BOX: return gslack_core<FamBox>(p, b, out);
+        case GK_CH6F: return gslack_core<FamCh6F>(p, b, out);
+        case GK_CH6FT: return gslack_core<FamCh6FT>(p, b, out);
+        case GK_CH3: return gslack_core<FamCh3>(p, b, out);
+        case GK_CH3T: return gslack_core<FamCh3T>(p, b, out);
+        case GK_CENT: return gslack_core<FamCent>(p, b, out);
+        case GK_BOXT: return gslack_core<FamBoxT>(p, b, out);
+    }
+    return capi_fail(MF_ERR_UNSUPPORTED, "no kernel instantiation");
 }
 
 extern "C" int mf_gdebug_duals(mf_gproblem *p, int b, double *out) {

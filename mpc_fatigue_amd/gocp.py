@@ -255,6 +255,37 @@ class GOCP:
         _lib.check(_lib.lib().mf_gdebug_counters(self._h, int(b), _lib.iptr(out)))
         return dict(zip(self.COUNTERS, (int(v) for v in out)))
 
+    KERNELS = ("k_geval", "k_gasm", "k_gpre", "k_gkkt", "k_gls")
+
+    def timing(self, enable: bool = True) -> None:
+        """Per-phase HIP-event timing of the next solves on this handle (mf_gproblem_timing; resets the totals)."""
+        _lib.check(_lib.lib().mf_gproblem_timing(self._h, int(enable)))
+
+    def kernel_stats(self) -> dict:
+        """{phase: (total ms, launches)} since timing(True)."""
+        ms, n, ne = (C.c_double * 5)(), (C.c_long * 5)(), C.c_longlong(0)
+        _lib.check(_lib.lib().mf_gproblem_kernel_stats(self._h, ms, n, C.byref(ne)))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.KERNELS)}
+
+    def node_evals(self) -> int:
+        """Node evaluations k_geval made since timing(True) (device-counted)."""
+        ms, n, ne = (C.c_double * 5)(), (C.c_long * 5)(), C.c_longlong(0)
+        _lib.check(_lib.lib().mf_gproblem_kernel_stats(self._h, ms, n, C.byref(ne)))
+        return int(ne.value)
+
+    def point(self, b: int = 0) -> tuple[np.ndarray, np.ndarray]:
+        """(slacks (N x ni), duals [lam | yi | ye | zxL | zxU | zuL | zuU | vL | vU]) of problem b after the last solve
+        (mf_gdebug_slacks / mf_gdebug_duals): with the solution vector, the primal-dual point an oracle-side KKT check
+        takes."""
+        N = self.N
+        s = np.zeros(N * max(1, self.ni))
+        _lib.check(_lib.lib().mf_gdebug_slacks(self._h, int(b), _lib.dptr(s)))
+        nd = N * self.nx + 3 * N * max(1, self.ni) + N * max(1, self.ne + self.nem) + 2 * (N + 1) * self.nx \
+            + 2 * N * self.nu + 1
+        d = np.zeros(nd + 64)
+        n = _lib.check(_lib.lib().mf_gdebug_duals(self._h, int(b), _lib.dptr(d)))
+        return s[:N * self.ni], d[:n - 1]
+
     def q_traj(self, w: np.ndarray) -> np.ndarray:
         """State trajectory x_0..x_N (N+1, nx) of a solution vector."""
         nx, nu, N = self.nx, self.nu, self.N

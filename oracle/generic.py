@@ -58,7 +58,9 @@ class GOpts(C.Structure):
                 ("u_init", C.POINTER(C.c_double)), ("max_soc", C.c_int), ("dual_out", C.POINTER(C.c_double)),
                 ("node_cb", C.c_void_p), ("node_ctx", C.c_void_p), ("val_cb", C.c_void_p),
                 ("warm_start", C.c_int), ("dual_in", C.POINTER(C.c_double)), ("riccati", C.c_int),
-                ("filter", C.c_int), ("dc_all", C.c_int), ("resto_hard_dyn", C.c_int)]
+                ("filter", C.c_int), ("dc_all", C.c_int), ("resto_hard_dyn", C.c_int),
+                ("kkt_at", C.c_int), ("s_in", C.POINTER(C.c_double)), ("kkt_out", C.POINTER(C.c_double)),
+                ("s_out", C.POINTER(C.c_double))]
 
 
 _lib = None
@@ -227,7 +229,7 @@ def w_size(g: GOCP) -> int:
 
 def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=False, verbose=0, F_init=0.0,
          w0=None, bound_relax=0.0, u_init=None, max_soc=0, dual_out=None, node_cb=None, node_ctx=None, val_cb=None,
-         warm_start=False, dual_in=None, riccati=False, filter=False, dc_all=False, resto_hard_dyn=False):
+         warm_start=False, dual_in=None, riccati=False, filter=False, dc_all=False, resto_hard_dyn=False, s_out=None):
     """mfg_opts (oracle/mf_ocp.c).  riccati: 0 block-tridiagonal KKT, 1 the device's Riccati recursion
     (banded in the restoration phase), 2 Riccati in the restoration phase too (relaxed dynamics rows,
     ric_relax), 3 test mode: both in the restoration phase, step difference in mfg_ric_check_max."""
@@ -240,6 +242,9 @@ def opts(tol=1e-8, constr_viol_tol=1e-8, max_iter=300, mu_init=0.1, init_zero=Fa
     if dual_out is not None:
         o._d = dual_out
         o.dual_out = _p(dual_out)
+    if s_out is not None:
+        o._so = s_out
+        o.s_out = _p(s_out)
     if u_init is not None:
         o._u_init = np.ascontiguousarray(u_init, dtype=np.float64)
         o.u_init = _p(o._u_init)
@@ -258,6 +263,33 @@ def solve(spec: dict, **kw):
     if err:
         raise RuntimeError(f"mfg_solve error {err}")
     return w, r
+
+
+KKT_KEYS = ("E0", "dinf", "pinf", "cinf0", "sd", "sc", "obj")
+
+
+def kkt_at(spec: dict, w, s, duals, L=None, **kw) -> dict:
+    """The oracle's own optimality measures at a given primal-dual point (no solve; mfg_opts.kkt_at): w in the
+    reference layout, s the slack rows (N x ni), duals in the dual_out layout [lam | yi | ye | zxL | zxU | zuL | zuU
+    | vL | vU] (a trailing mu is ignored).  E0 is IPOPT's scaled optimality error at mu = 0 with the
+    bound relaxation of kw (bound_relax) applied as in the solve.  Returns dict over KKT_KEYS."""
+    g, (b0, b1) = make(spec)
+    op = opts(**kw)
+    op.kkt_at = 1
+    op._w0 = np.ascontiguousarray(w, dtype=np.float64)
+    op.w0 = _p(op._w0)
+    op._si = np.ascontiguousarray(s, dtype=np.float64)
+    op.s_in = _p(op._si)
+    op._di = np.ascontiguousarray(duals, dtype=np.float64)
+    op.dual_in = _p(op._di)
+    out = np.zeros(8)
+    op.kkt_out = _p(out)
+    r = O.Result()
+    wd = np.zeros(w_size(g))
+    err = (L or lib()).mfg_solve(_p(b0), _p(b1), C.byref(g), C.byref(op), _p(wd), C.byref(r))
+    if err:
+        raise RuntimeError(f"mfg_solve error {err}")
+    return dict(zip(KKT_KEYS, (float(v) for v in out)))
 
 
 def bind(L):

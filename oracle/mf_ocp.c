@@ -141,6 +141,14 @@ typedef struct {
     /* 1: the restoration problem keeps the dynamics rows exact (elastic p, n only on the slack and
      * equality rows): the variant the device solver's stage-wise Riccati factorisation runs */
     int resto_hard_dyn;
+    /* 1: no solve -- the KKT measures of the given primal-dual point (tests: the oracle's own check of a device
+     * solution).  x, u from w0 exactly (no bound push), slacks from s_in (N x ni), multipliers from dual_in
+     * exactly (dual_out layout); kkt_out = [E_0 (mu = 0), dual inf., primal inf., complementarity, s_d, s_c,
+     * objective]; the problem as solved (bound_relax applies) */
+    int kkt_at;
+    const double *s_in;
+    double *kkt_out;
+    double *s_out;  /* diagnostics: the slack rows at the end (N x ni) or NULL */
 } mfg_opts;
 
 typedef struct {
@@ -2023,8 +2031,10 @@ static int resto_phase(ws_t *S, fst_t *Fm, double thc, int *it, fcount_t *C) {
 }
 
 /* IpoptAlgorithm::Optimize in filter mode: the main problem (R == NULL) or the restoration problem.
- * Returns 0 converged (resto: the original filter accepted), 1 max_iter, 3 inertia / restoration failure,
- * 4 restoration converged to a point of local infeasibility. */
+ * Returns the device's status codes (csrc/gipm.hip GS_*): 0 converged (resto: the original filter accepted),
+ * 1 max_iter, 3 inertia correction failed, 4 restoration failure (the restoration problem's line search failed:
+ * IPOPT's RESTORATION_FAILURE), 5 the restoration converged to a point of local infeasibility (IPOPT's
+ * LOCAL_INFEASIBILITY). */
 static int ipm_filter(ws_t *S, fst_t *F, int *it, fcount_t *C, const resto_ctx *R) {
     const mfg_opts *O = S->O;
     const double kappa_eps = 10.0, kappa_mu = 0.2, theta_mu = 1.5, tau_min = 0.99;
@@ -2050,7 +2060,7 @@ static int ipm_filter(ws_t *S, fst_t *F, int *it, fcount_t *C, const resto_ctx *
             merit_parts(S, S->x, S->u, S->s, R->mu_orig, &ph, &th, &ok, NULL, NULL, NULL);
             if (O->verbose) fprintf(stderr, "   orig theta %.4e (resto start %.4e) phi %.8e\n", th, R->th_R, ph);
             if (ok && th <= 0.9 * R->th_R && ls_orig_ok(R->LSo, ph, th)) return 0;
-            if (E0 <= O->tol) return 4;
+            if (E0 <= O->tol) return 5;
         }
         if (*it == O->max_iter) return 1;
         while (Emu <= kappa_eps * F->mu && F->mu > mu_min) {
@@ -2093,7 +2103,7 @@ static int ipm_filter(ws_t *S, fst_t *F, int *it, fcount_t *C, const resto_ctx *
                 continue;
             }
             F->in_soft = 0;
-            if (R) return 3;
+            if (R) return 4;
             F->n_resto++;
             const int st = resto_phase(S, F, thc, it, C);
             if (st) return st;
@@ -2140,7 +2150,7 @@ static int ipm_filter(ws_t *S, fst_t *F, int *it, fcount_t *C, const resto_ctx *
                     ap, az, alpha, accepted, soc_used, n_steps, F->in_wd, F->wd_trial, F->LS.nf, thc, phc);
         if (!accepted) {
             C->n_ls_fail++;
-            if (R) return 3;  /* no restoration inside the restoration phase */
+            if (R) return 4;  /* no restoration inside the restoration phase */
             /* PrepareRestoPhaseStart augments the filter with the current point; then the soft restoration
              * phase is tried, and the restoration phase if its step fails */
             F->LS.rph = phc; F->LS.rth = thc; F->LS.rgd = gdc;
@@ -2320,7 +2330,32 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
     const int has_tier1 = P->tier1_to > P->tier1_from;
 
     double ts[5] = {0, 0, 0, 0, 0}, t_solve0 = wall_s(), t_ph;
-    if (O->filter) {  /* IPOPT's globalisation (mfg_opts.filter) */
+    if (O->kkt_at) {  /* the KKT measures at the given point (mfg_opts.kkt_at) */
+        const int st = nu + nx;
+        for (int k = 0; k < N; k++) {
+            const double *wk = O->w0 + nx + (size_t)k * st;
+            for (int j = 0; j < nu; j++)
+                if (!S->ufix[k * nu + j]) S->u[k * nu + j] = wk[j];
+            for (int j = 0; j < nx; j++) S->x[(k + 1) * nx + j] = wk[nu + j];
+        }
+        memcpy(S->s, O->s_in, NI * sizeof(double));
+        const double *o = O->dual_in;
+        double *dst[] = {S->lam, S->yi, S->ye, S->zxL, S->zxU, S->zuL, S->zuU, S->vL, S->vU};
+        const size_t len[] = {(size_t)N * nx, NI, NE, NX1, NX1, NU, NU, NI, NI};
+        for (int a = 0; a < 9; a++) {
+            memcpy(dst[a], o, len[a] * sizeof(double));
+            o += len[a];
+        }
+        eval_all(S, ts);
+        errs_t Ek;
+        opt_error_f(S, 0.0, &Ek);
+        double fo = 0.0;
+        for (int k = 0; k < N; k++) fo += S->l[k];
+        double *ko = O->kkt_out;
+        ko[0] = fmax(fmax(Ek.dinf / Ek.sd, Ek.pinf), Ek.cinf0 / Ek.sc);
+        ko[1] = Ek.dinf; ko[2] = Ek.pinf; ko[3] = Ek.cinf0; ko[4] = Ek.sd; ko[5] = Ek.sc; ko[6] = fo;
+        status = 0; it = 0; E0 = ko[0]; cviol = Ek.pinf;
+    } else if (O->filter) {  /* IPOPT's globalisation (mfg_opts.filter) */
         fcount_t C;
         memset(&C, 0, sizeof C);
         C.nit = NIT4; C.E0 = INFINITY; C.cviol = INFINITY;
@@ -2629,6 +2664,7 @@ int mfg_solve(const double *blob0, const double *blob1, const mfg_ocp *P, const 
         res->n_ls_fail = n_ls_fail; res->n_inertia_fix = n_ic;
     }
     if (O->verbose) fprintf(stderr, "second-order corrections accepted: %d\n", n_soc);
+    if (O->s_out) memcpy(O->s_out, S->s, NI * sizeof(double));
     if (O->dual_out) {
         double *o = O->dual_out;
         const double *src[] = {S->lam, S->yi, S->ye, S->zxL, S->zxU, S->zuL, S->zuU, S->vL, S->vU};

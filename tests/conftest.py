@@ -22,17 +22,6 @@ def has_gpu() -> bool:
         return False
 
 
-@pytest.fixture(scope="session", autouse=True)
-def _torch_hip_runtime_first():
-    """Two HIP runtimes share a GPU test process: torch's bundled one and the ROCm one libmpcfatigue.so links.  torch's
-    initialises only if it comes first (a torch tensor created after a library solve in a fresh process fails with
-    "No HIP GPUs are available"), so GPU sessions initialise it before any test runs."""
-    if has_gpu():
-        import torch
-        torch.cuda.init()
-    yield
-
-
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

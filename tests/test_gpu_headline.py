@@ -1,0 +1,66 @@
+"""The headline workload on the GPU as the reference solves it: C2 (force_optimization_pilz_6DOF.py)
+by IPOPT from x0 = 0 -- filter line search, watchdog, soft restoration, the restoration phase with elastic rows,
+bound_relax_factor 1e-8, max_iter 3000 (csrc/gipm.hip, chain family) -- against the oracle in the same mode with the
+device's elimination (oracle/mf_ocp.c, riccati = 2).
+
+* 64 horizons of bench.py's C5 batch (N = 100) against the oracle's solves (fixture made by
+  tests/golden/make_c2_headline_fixture.py): every device point passes the oracle's own KKT check (E_0 <= 1e-8 at the
+  device's primal-dual point), the objective equals the oracle's to 1e-8 relative, nodes 0..N-1 to 1e-6 rad, and the
+  last node is the oracle's or its exact mirror image (tests/c2check.py); on identical paths the iterations agree +-2.
+* the reference's own C2 instance (15 Nm fatigue floor, L84-89) at the script's N = 60 and BASELINE's N = 100: the
+  device returns IPOPT's outcome for it, the same as the oracle's, at the same iteration count +-2.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from mpc_fatigue_amd import problems as PR
+from oracle import generic as G
+from tests import c2check
+from tests.conftest import GOLDEN, has_gpu
+
+pytestmark = pytest.mark.gpu
+
+if has_gpu():
+    from mpc_fatigue_amd.gocp import GOCP
+
+IPOPT_MODE = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=3000, max_soc=4)
+
+
+def test_headline_config_c2_n100_matches_oracle():
+    fx = np.load(os.path.join(GOLDEN, "c2_headline_ipopt_oracle.npz"))
+    Q0, LR = fx["q0"], fx["line_ref"]
+    B = Q0.shape[0]
+    np.testing.assert_array_equal(Q0, PR.pilz6_batch_q0(B, seed=0))  # bench.py's batch, first B horizons
+    base = PR.pilz6_bench(N=100)
+    g = GOCP(base)
+    r = g.solve(x0=Q0, line_ref=LR, **IPOPT_MODE)
+    n_same = n_mirror = 0
+    for b in range(B):
+        assert int(r.status[b]) == int(fx["status"][b]) == 0, (b, int(r.status[b]), int(fx["status"][b]))
+        spec = PR.pilz6_bench(N=100, q0=Q0[b], line_ref=LR[b])
+        c = c2check.check_solution(g, b, spec, r.w[b], float(r.obj[b]), fx["w"][b], float(fx["obj"][b]))
+        if c["same"]:
+            n_same += 1
+            if c["dq"] <= 1e-6 and int(r.iters[b]) != int(fx["iters"][b]):
+                print(f"horizon {b}: same point, iterations {int(r.iters[b])} vs {int(fx['iters'][b])}")
+        n_mirror += c["mirror"]
+        print(f"horizon {b}: device {int(r.iters[b])} it, oracle {int(fx['iters'][b])} it, E0 {c['E0']:.1e}, "
+              f"dobj {c['dobj']:.1e}, dq(0..N-1) {c['inner_dq']:.1e}, dq {c['dq']:.1e}, "
+              f"{'same' if c['same'] else 'mirror'}")
+    print(f"same last node: {n_same}, mirror image: {n_mirror} of {B}")
+    assert n_same + n_mirror == B
+
+
+@pytest.mark.parametrize("N", [60, 100])
+def test_reference_15nm_instance_same_ipopt_outcome(N):
+    spec = PR.pilz6_force(N=N)  # the reference's floor, 15 Nm
+    g = GOCP(spec)
+    r = g.solve(x0=np.asarray(spec["q0"])[None], **IPOPT_MODE)
+    _, ro = G.solve(spec, riccati=2, **IPOPT_MODE)
+    print(f"N={N}: device status {int(r.status[0])} after {int(r.iters[0])} iterations; oracle status {ro.status} "
+          f"after {ro.iter}; counters {g.counters(0)}")
+    assert int(r.status[0]) == ro.status
+    assert ro.status != 0
+    assert abs(int(r.iters[0]) - ro.iter) <= 2, (int(r.iters[0]), ro.iter)

@@ -1,0 +1,69 @@
+"""C2 solved as the reference solves it (IPOPT mode from x0 = 0, force_optimization_pilz_6DOF.py:195-197) on the
+first B horizons of the C5 batch: time, status counts, iteration distribution, per-horizon solver counters and the
+running-count trajectory (verbose host log with timestamps on stderr).
+
+    python tools/c2_ipopt_probe.py [B] [--max-iter 3000] [--reps 1] [--counters]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("batch", type=int, nargs="?", default=8192)
+    ap.add_argument("--max-iter", type=int, default=3000)
+    ap.add_argument("--reps", type=int, default=1)
+    ap.add_argument("--counters", action="store_true")
+    ap.add_argument("--verbose", type=int, default=1)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.init()
+    from mpc_fatigue_amd import pin, problems as PR
+    from mpc_fatigue_amd.gocp import GOCP
+    dev = torch.device("cuda", 0)
+    B = a.batch
+    sp = PR.pilz6_bench(N=100)
+    Q = PR.pilz6_batch_q0(B, seed=0)
+    lr = pin.generate_forward_kin(PR.read_urdf(sp["urdf"]), sp["frame"]).batch(Q)[0][:, :2]
+    g = GOCP(sp)
+    x = torch.as_tensor(Q, dtype=torch.float64, device=dev).contiguous()
+    l = torch.as_tensor(np.ascontiguousarray(lr), dtype=torch.float64, device=dev).contiguous()
+    out = {"w": torch.empty((B, g.wsize), dtype=torch.float64, device=dev),
+           "status": torch.empty(B, dtype=torch.int32, device=dev), "iters": torch.empty(B, dtype=torch.int32, device=dev),
+           "kkt": torch.empty(B, dtype=torch.float64, device=dev), "obj": torch.empty(B, dtype=torch.float64, device=dev)}
+    ptr = {k: v.data_ptr() for k, v in out.items()}
+    kw = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=a.max_iter, max_soc=4)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    g.solve_dev(x.data_ptr(), None, None, l.data_ptr(), B, ptr, stream=s, **dict(kw, max_iter=1))
+    torch.cuda.synchronize()
+    ts = []
+    for r in range(a.reps):
+        t0 = time.perf_counter()
+        g.solve_dev(x.data_ptr(), None, None, l.data_ptr(), B, ptr, stream=s, verbose=a.verbose if r == 0 else 0, **kw)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    st = out["status"].cpu().numpy()
+    it = out["iters"].cpu().numpy()
+    sv, sc = np.unique(st, return_counts=True)
+    rec = {"batch": B, "seconds": ts, "horizons_per_s": float((st == 0).sum() / np.median(ts)),
+           "status_counts": {int(k): int(v) for k, v in zip(sv, sc)},
+           "iters_mean": float(it.mean()), "iters_pct": {p: float(np.percentile(it, p)) for p in (50, 90, 99, 99.9, 100)}}
+    if a.counters:
+        C = np.array([list(g.counters(b).values()) for b in range(B)])
+        rec["counters_mean"] = dict(zip(GOCP.COUNTERS, (float(v) for v in C.mean(0))))
+        rec["resto_iter_share"] = float(C[:, 9].sum() / max(1, C[:, 0].sum()))
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main()
