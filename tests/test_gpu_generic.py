@@ -504,12 +504,14 @@ def test_c2_ipopt_mode_sixteen_horizons_match_oracle():
     same = 0
     for b in range(len(idx)):
         assert int(r.status[b]) == R[b].status == 0, (idx[b], int(r.status[b]), R[b].status)
-        c = c2check.check_solution(g, b, specs[b], r.w[b], float(r.obj[b]), W[b], R[b].obj)
+        c = c2check.compare(g, b, specs[b], r.w[b], float(r.obj[b]), W[b], R[b].obj, q_tol=1e-5)
         print(f"start {idx[b]}: device {int(r.iters[b])} it, oracle {R[b].iter} it, E0 {c['E0']:.1e}, dobj {c['dobj']:.1e}, "
-              f"dq(0..N-1) {c['inner_dq']:.1e}, dq {c['dq']:.1e}, {'same' if c['same'] else 'mirror'}")
-        if int(r.iters[b]) == R[b].iter:
-            same += 1
-    print("identical iteration counts:", same, "of", len(idx))
+              f"dq(0..N-1) {c['inner_dq']:.1e}, dq {c['dq']:.1e}, {c['kind']}")
+        assert c["E0"] <= 1e-8 and c["pinf"] <= 1e-8, (idx[b], c)
+        assert c["dobj"] <= (1e-12 if c["kind"] != "neighbour" else 1e-5), (idx[b], c)
+        same += c["kind"] != "neighbour"
+    print("the oracle's optimum:", same, "of", len(idx))
+    assert same >= len(idx) // 2
 
 
 def test_c2_ipopt_restoration_with_elastic_dynamics_rows():
@@ -545,8 +547,13 @@ def test_c2_ipopt_restoration_with_elastic_dynamics_rows():
         m = meta[f"C2_{i}"]
         assert int(r.status[b]) == 0, (i, int(r.status[b]), int(r.iters[b]))
         spec = PR.pilz6_bench(N=100, q0=Q0[b], line_ref=LR[b])
-        c = c2check.check_solution(g, b, spec, r.w[b], float(r.obj[b]), w_or, m["obj"])
+        c = c2check.compare(g, b, spec, r.w[b], float(r.obj[b]), w_or, m["obj"], q_tol=1e-5)
         print(f"horizon {i}: device {int(r.iters[b])} it, oracle {m['iter']} it, {c}")
+        assert c["E0"] <= 1e-8 and c["pinf"] <= 1e-8, (i, c)
+        if i == 45:  # the oracle's path exactly (r05, r06d)
+            assert c["kind"] == "same" and c["dobj"] <= 1e-12 and int(r.iters[b]) == m["iter"], (i, c)
+        else:  # 41, 48: the paths part inside a restoration phase; neighbouring optima (r06d: dobj 2.2e-6, 5.0e-6)
+            assert c["dobj"] <= 1e-5, (i, c)
 
 
 @pytest.mark.parametrize("case", ["c3", "c4", "c2"])
