@@ -24,6 +24,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -118,6 +119,7 @@ struct GArrays {
     int *pidx, *next, *init;
     int total;
     unsigned long long *neval;  // timing mode (mf_gproblem_timing): node evaluations made by k_geval, else nullptr
+    int fast_kkt;               // k_gkkt_chain ran before this k_gkkt launch: skip the horizons it took
     const double *x0all, *lrall;  // every problem's x_0 and line reference (total rows)
     double *ow, *okkt, *oobj;     // every problem's outputs
     int *ost, *oit;
@@ -509,11 +511,18 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     constexpr int NX = D::NX, NU = D::NU, NV = D::NV, NI = D::NI, NE = D::NE, NIA = D::NIA, NEA = D::NEA;
     constexpr int NM = D::NM, NET = D::NET;  // mixed rows c_m(x_k, u_k): multipliers at ye[k NET + NEA + m]
     constexpr int NK = NU + NET, LDK = NK + 1;
-    const int lane = threadIdx.x;
+    // (not const: the serial stage loops redefine it opaquely per stage, so the per-lane addresses are recomputed
+    // inside them instead of being hoisted out and held in registers across the sweep)
+    int lane = threadIdx.x;
     // PH 3 (k_gspec): block s GNSPEC + t is try t of the s-th running horizon, with factor storage row blockIdx.x
     const int b = PH == 3 ? (blockIdx.x < GNSPEC * A.spec_max ? A.slist[blockIdx.x / GNSPEC] : -1) : (int)blockIdx.x;
     if (b < 0 || b >= batch) return;
-    GState st = A.st[b];
+    // the horizon's state in LDS: a register copy of GState (~70 dwords) stays live across the whole phase body; every
+    // lane reads the same values and the uniform updates below are the same store from every lane
+    __shared__ GState st_lds;
+    if (lane == 0) st_lds = A.st[b];
+    wave_lds_sync();
+    GState &st = st_lds;
     if (st.status != GS_RUNNING) {
         if (PH == 3 && lane == 0) A.sres[blockIdx.x] = -1;
         return;
@@ -1151,6 +1160,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         for (int e = lane; e < NX * NX; e += 64) Ps[e] = (e / NX == e % NX) ? Sx[N * NX + e / NX] + dw : 0.0;
         __syncthreads();
         for (int k = N - 1; k >= 0; k--) {
+            lane = lane_opaque();
             GSTAMP(2);
             const bool en = eqon(k + 1);
             if (rlx && relax_stage(k, en)) return 1;
@@ -1348,6 +1358,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         for (int j = lane; j < NX; j += 64) pvs[j] = gx[N * NX + j] - lam[(N - 1) * NX + j];
         gsync();
         for (int k = N - 1; k >= 0; k--) {
+            lane = lane_opaque();
             const double *rk = R(k);
             const bool en = eqon(k + 1);
             GSTAMP(26);
@@ -1490,6 +1501,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         for (int ee = lane; ee < NEA; ee += 64) dye[ee] = 0.0;  // state rows of node 0 (inactive)
         gsync();
         for (int k = 0; k < N; k++) {
+            lane = lane_opaque();
             const double *rk = R(k);
             const bool en = eqon(k + 1);
             // the stage's operands into LDS first (one round trip), then three LDS-only phases
@@ -1810,6 +1822,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
 
     if constexpr (PH == 1) {
     if (flt && (st.pend == GP_IDLE || st.pend == GP_IDLE_RESTO || st.pend == GP_WDSOFT)) return;
+    if (flt && A.fast_kkt && st.mode == 0 && st.pend == GP_NONE) return;  // taken by k_gkkt_chain (gkkt_chain.hpp)
     // a try k_gspec has made with exactly these parameters: its result, and on success the direction (and the line
     // search's corrections, st.frow) use its factors where they lie
     const int srow = (flt && !lsm && A.spec_of) ? A.spec_of[b] : -1;
@@ -2408,6 +2421,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(OCC))) void 
     giter_phase<FAM, 2, FLT>(M0, M1, F0, F1, P, A, batch);
 }
 
+}  // namespace mf
+#include "gkkt_chain.hpp"
+namespace mf {
+
 // ============================================================== outputs
 template <class D>
 __global__ void k_gout(GArrays A, int N, int batch, double *w, int *status, int *iters, double *kkt, double *obj) {
@@ -2751,6 +2768,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     A.pidx = A.next = A.init = nullptr;
     A.total = total;
     A.neval = nullptr;
+    A.fast_kkt = 0;
     if (p->timing) {
         if (!p->d_neval) {
             GHIPCHK(hipMalloc(&p->d_neval, sizeof(unsigned long long)));
@@ -2817,6 +2835,13 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     }
     if (o && o->verbose && spec_ok) fprintf(stderr, "[mf gipm] concurrent inertia tries from %d running horizons\n", A.spec_max);
     GArrays As = A;  // k_gkkt's view: spec_of set while k_gspec runs
+    // the chain family's main-problem Newton step by k_gkkt_chain (IPOPT mode, not while k_gspec runs);
+    // MF_CHAIN_KKT=0 in the environment keeps k_gkkt for every horizon (A/B diagnostics)
+    bool chain_kkt = false;
+    if constexpr (ChainEuler<FAM>::value) {
+        const char *ev = getenv("MF_CHAIN_KKT");
+        chain_kkt = P.filter && !(ev && ev[0] == '0');
+    }
     // the occupancy variants while more horizons run than the default kernels hold (four per CU; measured on the C2
     // leg: launches at ~1000 running horizons take the same time with either k_gkkt, fewer run faster without spills)
     int kkt_occ_from = batch;
@@ -2851,6 +2876,13 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             hipLaunchKernelGGL(k_gpre<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, A, batch);
             mark(c, 2, 1);
             mark(c, 3, 0);
+            As.fast_kkt = 0;
+            if constexpr (ChainEuler<FAM>::value) {
+                if (chain_kkt && !spec) {
+                    hipLaunchKernelGGL(k_gkkt_chain<FAM>, dim3(batch), dim3(64), 0, s, P, A, batch);
+                    As.fast_kkt = 1;
+                }
+            }
             if (spec) {
                 hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch);
                 hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * std::min(active, A.spec_max)), dim3(64), 0, s, M0, M1, F0,

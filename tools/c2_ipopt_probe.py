@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=1)
     ap.add_argument("--counters", action="store_true")
     ap.add_argument("--verbose", type=int, default=1)
+    ap.add_argument("--timing", action="store_true", help="per-phase HIP-event timing of the (first) timed solve")
     a = ap.parse_args()
     import torch
     torch.cuda.init()
@@ -47,6 +48,8 @@ def main():
     g.solve_dev(x.data_ptr(), None, None, l.data_ptr(), B, ptr, stream=s, **dict(kw, max_iter=1))
     torch.cuda.synchronize()
     ts = []
+    if a.timing:
+        g.timing(True)
     for r in range(a.reps):
         t0 = time.perf_counter()
         g.solve_dev(x.data_ptr(), None, None, l.data_ptr(), B, ptr, stream=s, verbose=a.verbose if r == 0 else 0, **kw)
@@ -58,6 +61,10 @@ def main():
     rec = {"batch": B, "seconds": ts, "horizons_per_s": float((st == 0).sum() / np.median(ts)),
            "status_counts": {int(k): int(v) for k, v in zip(sv, sc)},
            "iters_mean": float(it.mean()), "iters_pct": {p: float(np.percentile(it, p)) for p in (50, 90, 99, 99.9, 100)}}
+    if a.timing:
+        rec["kernel_ms"] = {k: round(v[0], 1) for k, v in g.kernel_stats().items()}
+        rec["node_evals"] = g.node_evals()
+        g.timing(False)
     if a.counters:
         C = np.array([list(g.counters(b).values()) for b in range(B)])
         rec["counters_mean"] = dict(zip(GOCP.COUNTERS, (float(v) for v in C.mean(0))))
