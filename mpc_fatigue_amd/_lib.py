@@ -164,6 +164,7 @@ def lib() -> C.CDLL:
         "mf_gnode_record": ([vp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
         "mf_gdebug_duals": ([vp, C.c_int, dp], C.c_int),
         "mf_gdebug_slacks": ([vp, C.c_int, dp], C.c_int),
+        "mf_debug_bk_compare": ([dp, C.c_int, dp, dp, ip], C.c_int),
         "mf_gproblem_timing": ([vp, C.c_int], C.c_int),
         "mf_gproblem_kernel_stats": ([vp, dp, C.POINTER(C.c_long), C.POINTER(C.c_longlong)], C.c_int),
         "mf_gdebug_counters": ([vp, C.c_int, ip], C.c_int),
@@ -187,7 +188,7 @@ EXPORTED_SYMBOLS = [
     "mf_problem_kernel_stats", "mf_problem_trace", "mf_kernel_name", "mf_ik_batch", "mf_ik_batch_dev", "mf_last_error",
     "mf_gopts_init", "mf_gproblem_create", "mf_gproblem_free", "mf_gproblem_dims", "mf_gsolve_batch", "mf_gsolve_batch_dev",
     "mf_gsolve_stream_dev",
-    "mf_gnode_record", "mf_gdebug_duals", "mf_gdebug_slacks", "mf_gproblem_timing", "mf_gproblem_kernel_stats",
+    "mf_gnode_record", "mf_gdebug_duals", "mf_gdebug_slacks", "mf_debug_bk_compare", "mf_gproblem_timing", "mf_gproblem_kernel_stats",
     "mf_gdebug_counters", "mf_gdebug_trace", "mf_gdebug_trace_reset",
 ]
 

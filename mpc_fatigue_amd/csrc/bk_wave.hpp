@@ -166,7 +166,7 @@ __device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm,
                 int i = k + 1 + e / t, j = k + 1 + e % t;
                 if (j <= i) {
                     double ci = A[i * LD + k], cj = A[j * LD + k];
-                    double val = A[i * LD + j] - (ci * inv) * cj;
+                    double val = fma(-(ci * inv), cj, A[i * LD + j]);
                     A[i * LD + j] = val;
                     A[j * LD + i] = val;
                 }
@@ -180,7 +180,7 @@ __device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm,
             if (lane == 0) piv[k] = 1;
         } else {
             double a = A[k * LD + k], b = A[(k + 1) * LD + k], c = A[(k + 1) * LD + k + 1];
-            double det = a * c - b * b;
+            double det = fma(a, c, -(b * b));
             if (det < 0) { in.pos++; in.neg++; }
             else if (det > 0) { if (a + c > 0) in.pos += 2; else in.neg += 2; }
             else in.zero += 2;
@@ -191,8 +191,8 @@ __device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm,
                 if (j <= i) {
                     double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
                     double c0j = A[j * LD + k], c1j = A[j * LD + k + 1];
-                    double l0 = c0i * ia + c1i * ib, l1 = c0i * ib + c1i * ic;
-                    double val = A[i * LD + j] - (l0 * c0j + l1 * c1j);
+                    double l0 = fma(c0i, ia, c1i * ib), l1 = fma(c0i, ib, c1i * ic);
+                    double val = A[i * LD + j] - fma(l0, c0j, l1 * c1j);
                     A[i * LD + j] = val;
                     A[j * LD + i] = val;
                 }
@@ -200,7 +200,7 @@ __device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm,
             __syncthreads();
             for (int i = k + 2 + lane; i < m; i += 64) {
                 double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
-                double l0 = c0i * ia + c1i * ib, l1 = c0i * ib + c1i * ic;
+                double l0 = fma(c0i, ia, c1i * ib), l1 = fma(c0i, ib, c1i * ic);
                 A[i * LD + k] = l0;
                 A[i * LD + k + 1] = l1;
             }
@@ -640,7 +640,7 @@ __device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, B
                     const double ci = a[k];
 #pragma unroll
                     for (int j = k + 1; j < M; j++)
-                        if (j <= lane) a[j] = a[j] - (ci * inv) * r[j];
+                        if (j <= lane) a[j] = fma(-(ci * inv), r[j], a[j]);
                     a[k] = ci * inv;
                 }
             }
@@ -663,6 +663,168 @@ __device__ __forceinline__ bool bk_factor_regs(double *A, int *perm, int *piv, B
     in.neg = neg;
     in.zero = 0;
     return true;
+}
+
+// bk_factor_wave in registers with its pivoting (1x1 / 2x2 pivots, symmetric row and column swaps), for M <= 64:
+// lane i keeps row i of the whole matrix, the pivot searches are readlane scans (the first maximum, like the wave's
+// argmax), swaps exchange two lanes' rows and two register columns, and every arithmetic operation is the wave's in
+// the wave's order, so the lower triangle (L and D), perm, piv and the inertia are bit-identical to bk_factor_wave's.
+// The updates are written with explicit fma in both routines: left to contraction, an update under a per-lane select
+// (lower entry or mirrored one) is compiled as a select of two products and an unfused subtraction.
+// The wave routine keeps both triangles: an update writes the value it computes for (i, j), i >= j, to (j, i) as
+// well.  Lane i computes the upper entries of its row with the mirror's operands ((c_j / d) c_i for the 1x1 update,
+// from the mirror's own l_j for the 2x2), which gives the same bits once the block is symmetric.  The block as built
+// need not be symmetric to the last bit, and the first step reads it as the wave does (row imax's upper part in the
+// pivot test, upper entries moved below the diagonal by a swap); after that step the trailing block is made
+// symmetric by copying its lower triangle up, as the wave's first update does.
+template <int M>
+__device__ __forceinline__ double reg_sel(const double (&a)[M], int idx) {
+    double r = a[0];
+#pragma unroll
+    for (int j = 1; j < M; j++) r = (idx == j) ? a[j] : r;
+    return r;
+}
+template <int LD, int M>
+__device__ __forceinline__ BKInertia bk_factor_regs_piv(double *A, int *perm, int *piv) {
+    static_assert(M >= 2 && M <= 64, "one row per lane");
+    const int lane = lane_opaque();
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    double a[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) a[j] = A[min(lane, M - 1) * LD + j];
+    int pm = lane, pv = 1;
+    BKInertia in{0, 0, 0};
+    bool skip = false;
+#pragma unroll
+    for (int k = 0; k < M; k++) {
+        if (skip) {
+            skip = false;
+            continue;
+        }
+        const int k1 = k + 1 < M ? k + 1 : M - 1;  // (the second column of a 2x2 pivot; never k = M - 1)
+        double colmax = 0.0;
+        int imax = k;
+#pragma unroll
+        for (int i = k + 1; i < M; i++) {
+            const double v = fabs(readlane_d(a[k], i));
+            if (v > colmax) {
+                colmax = v;
+                imax = i;
+            }
+        }
+        const double absakk = fabs(readlane_d(a[k], k));
+        int kstep = 1, kp = k;
+        const bool zero = fmax(absakk, colmax) == 0.0;
+        if (zero) {
+            in.zero++;
+        } else {
+            if (!(absakk >= alpha * colmax)) {
+                double rowmax = 0.0, dmax = 0.0;
+#pragma unroll
+                for (int j = k; j < M; j++) {
+                    const double v = readlane_d(a[j], imax);
+                    if (j != imax) rowmax = fmax(rowmax, fabs(v));
+                    else dmax = v;
+                }
+                if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
+                else if (fabs(dmax) >= alpha * rowmax) kp = imax;
+                else { kp = imax; kstep = 2; }
+            }
+            const int kk = k + kstep - 1;
+            if (kp != kk) {
+                // rows kk <-> kp (two lanes), then columns kk <-> kp (every lane), then perm
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    const double vkk = readlane_d(a[j], kk), vkp = readlane_d(a[j], kp);
+                    a[j] = lane == kk ? vkp : (lane == kp ? vkk : a[j]);
+                }
+                const double tk = reg_sel(a, kk), tp = reg_sel(a, kp);
+#pragma unroll
+                for (int j = 0; j < M; j++) a[j] = j == kk ? tp : (j == kp ? tk : a[j]);
+                const int pk = __builtin_amdgcn_readlane(pm, kk), pp = __builtin_amdgcn_readlane(pm, kp);
+                pm = lane == kk ? pp : (lane == kp ? pk : pm);
+            }
+            if (kstep == 1) {
+                const double d = readlane_d(a[k], k);
+                if (d > 0) in.pos++;
+                else if (d < 0) in.neg++;
+                else in.zero++;
+                const double inv = 1.0 / d;
+                double c[M];
+#pragma unroll
+                for (int i = k + 1; i < M; i++) c[i] = readlane_d(a[k], i);
+                if (lane > k && lane < M) {
+                    const double ci = a[k];
+#pragma unroll
+                    for (int j = k + 1; j < M; j++) {
+                        if (j <= lane) a[j] = fma(-(ci * inv), c[j], a[j]);
+                        else if (k > 0) a[j] = fma(-(c[j] * inv), ci, a[j]);  // (j, lane)'s value
+                    }
+                    a[k] = ci * inv;
+                } else if (lane == k) {
+#pragma unroll
+                    for (int i = k + 1; i < M; i++) a[i] = c[i] * inv;  // row k: the L column mirrored
+                }
+                if (lane == k) pv = 1;
+            } else {
+                const double a2 = readlane_d(a[k], k), b = readlane_d(a[k], k1), c2 = readlane_d(a[k1], k1);
+                const double det = fma(a2, c2, -(b * b));
+                if (det < 0) { in.pos++; in.neg++; }
+                else if (det > 0) { if (a2 + c2 > 0) in.pos += 2; else in.neg += 2; }
+                else in.zero += 2;
+                const double ia = c2 / det, ib = -b / det, ic = a2 / det;
+                double c0[M], c1[M];
+#pragma unroll
+                for (int i = k + 2; i < M; i++) {
+                    c0[i] = readlane_d(a[k], i);
+                    c1[i] = readlane_d(a[k1], i);
+                }
+                if (lane >= k + 2 && lane < M) {
+                    const double c0i = a[k], c1i = a[k1];
+                    const double l0 = fma(c0i, ia, c1i * ib), l1 = fma(c0i, ib, c1i * ic);
+#pragma unroll
+                    for (int j = k + 2; j < M; j++) {
+                        if (j <= lane) {
+                            a[j] = a[j] - fma(l0, c0[j], l1 * c1[j]);
+                        } else if (k > 0) {
+                            const double l0j = fma(c0[j], ia, c1[j] * ib), l1j = fma(c0[j], ib, c1[j] * ic);
+                            a[j] = a[j] - fma(l0j, c0i, l1j * c1i);  // (j, lane)'s value
+                        }
+                    }
+                    a[k] = l0;
+                    a[k1] = l1;
+                }
+                if (lane == k) pv = 2;
+                if (lane == k1) pv = 0;
+                skip = true;
+            }
+        }
+        if (k == 0) {
+            // the trailing block symmetric from its lower triangle (the wave's first update wrote both triangles),
+            // through LDS: rows out, the upper part of each row back in from the columns below the diagonal
+            const int t0 = 1 + (kstep == 2 ? 1 : 0);
+            if (lane < M) {
+#pragma unroll
+                for (int j = 0; j < M; j++)
+                    if (j <= lane) A[lane * LD + j] = a[j];
+            }
+            wave_lds_sync();
+            if (lane >= t0 && lane < M) {
+#pragma unroll
+                for (int j = 1; j < M; j++)
+                    if (j > lane) a[j] = A[j * LD + lane];
+            }
+            wave_lds_sync();
+        }
+    }
+    if (lane < M) {
+#pragma unroll
+        for (int j = 0; j < M; j++) A[lane * LD + j] = a[j];
+        perm[lane] = pm;
+        piv[lane] = pv;
+    }
+    wave_lds_sync();
+    return in;
 }
 
 // Solve A X = B for nr right-hand sides; B is m x NR (row-major, LD NR) in LDS.

@@ -124,6 +124,34 @@ MF_HD void arm_values(const DevModel &M, const DevFrame &F, const double *q, con
     node_values<NJ>(M, F, F.parent, in, Fw, o);
 }
 
+// q direction v by the split sweep (adj.hpp node_fwd_rev_split): plain FP64 over the joints below v, Dual from v on
+template <int NJ> struct GLaneInSplit {
+    const double *xq, *xqd;
+    int v;
+    MF_HD Dual qd(int i) const { return Dual(xqd[i], 0.0); }
+    MF_HD void sincos(int i, double &s, double &c) const { sincos_t(xq[i], s, c); }
+    MF_HD void sincos(int i, Dual &s, Dual &c) const { sincos_t(Dual(xq[i], v == i ? 1.0 : 0.0), s, c); }
+};
+// C2's chain lanes (the specialised solver's eval arithmetic, csrc/ipm_kernels.hip k_eval_q / k_eval_node<..,1>):
+// q direction v by the split sweep -- its column is valid in the rows >= v of the q-q block (the rows above are
+// never read) -- and qd directions without the q-gradient adjoint (GQ = false: the q-qd block is read from the q
+// lanes' qd-gradient).  The force row is zeroed first: the split sweep does not emit it when the frame's parent
+// lies below v (the entry is exactly zero then).
+template <int NJ>
+MF_HD void arm_lane_split(const DevModel &M, const DevFrame &F, const double *q, const double *qd, const double *Fw,
+                          const double *c, const double *seed, int v, double *col) {
+    GLaneOut<NJ> o{col};
+#pragma unroll
+    for (int k = 0; k < 3; k++) col[GLaneOut<NJ>::HF + k] = 0.0;
+    if (v < NJ) {
+        GLaneInSplit<NJ> in{q, qd, v};
+        node_fwd_rev_split<NJ>(M, F, F.parent, v, in, Fw, c, seed, o);
+    } else {
+        GLaneIn<NJ, double> in{q, qd, v};
+        node_fwd_rev<double, Dual, NJ, true, false>(M, F, F.parent, in, Fw, c, seed, o);
+    }
+}
+
 template <int NJ>
 MF_HD void arm_lane(const DevModel &M, const DevFrame &F, const double *q, const double *qd, const double *Fw,
                     const double *c, const double *seed, int v, double *col) {
@@ -150,6 +178,7 @@ MF_HD double skew_el(const double *y, int r, int c) {  // [y]x (r, c)
 // fatigue budget sum_j T_j <= c_hi (build-defined extension of C3; parity unpinned).
 template <bool TH> struct BoxFamT {
     static constexpr int NJ = 6, NARM = 2, NDIR = 2 * NJ, NM = 2, NQ = 12;
+    static constexpr bool SPLIT = false;
     using D = GDims<TH ? 2 * NQ : NQ, 18, TH ? 19 : 18, 1>;
     static constexpr int NX = D::NX;
     static constexpr int LANES = NARM * NDIR;  // derivative lanes per node
@@ -425,6 +454,9 @@ using BoxThermFam = BoxFamT<true>;
 template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
     static constexpr int NJ = NJ_, NF = NF_, NDIR = 2 * NJ_, NM = 1;
     static constexpr bool TH = THERMAL_;
+    // C2 (6 joints, one force, the line rows, no thermal state): the split lanes (arm_lane_split), evaluated
+    // direction-major by k_geval_chain (csrc/gkkt_chain.hpp)
+    static constexpr bool SPLIT = NJ_ == 6 && NF_ == 1 && NE_ == 2 && !THERMAL_;
     using D = GDims<(THERMAL_ ? 2 : 1) * NJ_, NJ_ + NF_, NJ_, NE_>;
     static constexpr int LANES = NDIR;
     static constexpr int LCOL = GLaneOut<NJ>::LCOL;
@@ -494,7 +526,8 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
     }
     template <class MA, class FA> MF_HD static void lane(MA M, FA F, const double *x, const double *u, const double *, int v,
                            Scratch &S) {
-        arm_lane<NJ>(M[0], F[0], x, u, S.Fw, S.cw, S.seed, v, S.col[0][v]);
+        if constexpr (SPLIT) arm_lane_split<NJ>(M[0], F[0], x, u, S.Fw, S.cw, S.seed, v, S.col[0][v]);
+        else arm_lane<NJ>(M[0], F[0], x, u, S.Fw, S.cw, S.seed, v, S.col[0][v]);
     }
     // d tau_j / d(var)
     MF_HD static double dtau(const GParams &P, const Scratch &S, int j, int v) {
@@ -526,6 +559,9 @@ template <int NJ_, int NF_, int NE_, bool THERMAL_> struct ChainFam {
             const int dr = kr == 0 ? lr : NJ + lr, dc = kc == 0 ? lc : NJ + lc;
             if (kr == 2) w = colent(dc, kr, lr);
             else if (kc == 2) w = colent(dr, kc, lc);
+            else if (SPLIT && kr == 0 && kc == 0) w = lr >= lc ? colent(lc, 0, lr) : colent(lr, 0, lc);  // lower triangle
+            else if (SPLIT && kr == 0) w = colent(lr, 1, lc);  // the q_lr lane's qd-gradient
+            else if (SPLIT && kc == 0) w = colent(lc, 1, lr);
             else w = 0.5 * (colent(dc, kr, lr) + colent(dr, kc, lc));
         }
         if (kr != 3 && kc != 3) {
@@ -634,6 +670,7 @@ MF_HD void mul_abt(const double *A, const double *B, double *C) {
 
 struct CentauroFam {
     static constexpr int NJ = 7, NARM = 2, NDIR = 2 * NJ, NM = 2, NQ = 2 * NJ;
+    static constexpr bool SPLIT = false;
     using D = GDims<2 * NQ, NQ + 6, NQ, 6, 6>;
     static constexpr int LANES = NARM * NDIR;  // derivative lanes per node
     static constexpr int PRE = NARM;

@@ -2,7 +2,10 @@
 first B horizons of the C5 batch: time, status counts, iteration distribution, per-horizon solver counters and the
 running-count trajectory (verbose host log with timestamps on stderr).
 
-    python tools/c2_ipopt_probe.py [B] [--max-iter 3000] [--reps 1] [--counters]
+    python tools/c2_ipopt_probe.py [B] [--max-iter 3000] [--reps 1] [--counters] [--timing] [--cstamps]
+
+--cstamps runs the diagnostic build libmpcfatigue_cstamps.so (make -C mpc_fatigue_amd libmpcfatigue_cstamps.so) and
+reports k_gkkt_chain's per-phase cycle counts over the timed solve.
 """
 from __future__ import annotations
 
@@ -26,7 +29,10 @@ def main():
     ap.add_argument("--counters", action="store_true")
     ap.add_argument("--verbose", type=int, default=1)
     ap.add_argument("--timing", action="store_true", help="per-phase HIP-event timing of the (first) timed solve")
+    ap.add_argument("--cstamps", action="store_true", help="k_gkkt_chain phase cycles (diagnostic build)")
     a = ap.parse_args()
+    if a.cstamps:
+        os.environ["MF_LIB"] = "libmpcfatigue_cstamps.so"
     import torch
     torch.cuda.init()
     from mpc_fatigue_amd import pin, problems as PR
@@ -50,6 +56,11 @@ def main():
     ts = []
     if a.timing:
         g.timing(True)
+    if a.cstamps:
+        import ctypes
+        from mpc_fatigue_amd import _lib
+        L = _lib.lib()
+        assert L.mf_debug_cstamps_reset() == 0
     for r in range(a.reps):
         t0 = time.perf_counter()
         g.solve_dev(x.data_ptr(), None, None, l.data_ptr(), B, ptr, stream=s, verbose=a.verbose if r == 0 else 0, **kw)
@@ -65,6 +76,19 @@ def main():
         rec["kernel_ms"] = {k: round(v[0], 1) for k, v in g.kernel_stats().items()}
         rec["node_evals"] = g.node_evals()
         g.timing(False)
+    if a.cstamps:
+        cs = (ctypes.c_ulonglong * 16)()
+        assert L.mf_debug_cstamps(cs) == 0
+        cs = list(cs)
+        names = ["setup", "stage_loads", "slack_w_tv", "block_rows_vec", "bk_factor", "stores_solve", "p_update",
+                 "forward", "slack_mult"]
+        tot = sum(cs[:9]) + cs[12]
+        rec["cstamps"] = {"cycles_share": {n: round(cs[i] / max(1, tot), 4) for i, n in enumerate(names)},
+                          "sweeps": cs[9], "stages": cs[10], "launches": cs[11],
+                          "cycles_per_stage": {n: round(cs[i] / max(1, cs[10]), 1) for i, n in enumerate(names[1:7], 1)},
+                          "cycles_per_launch": round(tot / max(1, cs[11]), 1),
+                          "pivoted_factor": {"cycles_share": round(cs[12] / max(1, tot), 4), "count": cs[13]},
+                          "sweeps_wrong_inertia": cs[14], "sweeps_singular": cs[15]}
     if a.counters:
         C = np.array([list(g.counters(b).values()) for b in range(B)])
         rec["counters_mean"] = dict(zip(GOCP.COUNTERS, (float(v) for v in C.mean(0))))
