@@ -278,10 +278,11 @@ int mf_gdebug_duals(mf_gproblem *p, int b, double *out);
 /* Diagnostics: the slack rows s (N x ni, node-major) of problem b after the last solve -- with mf_gdebug_duals the
  * primal-dual point an oracle-side KKT check of a device solution needs.  Returns N x ni. */
 int mf_gdebug_slacks(mf_gproblem *p, int b, double *out);
-/* Diagnostics: n stage blocks of the C2 chain (M x (M + 1) row-major, M = 9) factorised on the device by the register
- * Bunch-Kaufman of k_gkkt_chain and by the LDS one of k_gkkt: the two factors (same layout) and per block
- * meta[2M + 6] = {perm | piv << 8 (M, registers), the same (M, LDS), inertia (pos, neg, zero) x 2}.  Returns M. */
-int mf_debug_bk_compare(const double *K, int n, double *out_regs, double *out_wave, int *meta);
+/* Diagnostics: n stage blocks of the C2 chain (M x (M + 1) row-major, M = 9) factorised on the device by a Bunch-Kaufman
+ * variant (0: registers with pivoting, 1: LDS with unrolled scans, 2: natural-order registers with variant 1 as
+ * fallback (k_gkkt_chain), 3: registers with pivoting, runtime step loop) and by the LDS routine of k_gkkt: the two factors (same layout) and per block
+ * meta[2M + 6] = {perm | piv << 8 (M, variant), the same (M, k_gkkt's), inertia (pos, neg, zero) x 2}.  Returns M. */
+int mf_debug_bk_compare(const double *K, int n, int variant, double *out_var, double *out_wave, int *meta);
 /* Per-phase timing of the generic solver (HIP events on the solve stream around every launch group; bench.py):
  * enable != 0 turns it on and resets the accumulators.  kernel_stats: total ms and launches per slot
  * {k_geval, k_gasm, k_gpre, k_gkkt (with k_gspec and the occupancy variant), k_gls}, and (node_evals, may be

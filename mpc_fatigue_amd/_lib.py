@@ -164,7 +164,7 @@ def lib() -> C.CDLL:
         "mf_gnode_record": ([vp, dp, dp, dp, dp, dp, dp, C.c_int], C.c_int),
         "mf_gdebug_duals": ([vp, C.c_int, dp], C.c_int),
         "mf_gdebug_slacks": ([vp, C.c_int, dp], C.c_int),
-        "mf_debug_bk_compare": ([dp, C.c_int, dp, dp, ip], C.c_int),
+        "mf_debug_bk_compare": ([dp, C.c_int, C.c_int, dp, dp, ip], C.c_int),
         "mf_gproblem_timing": ([vp, C.c_int], C.c_int),
         "mf_gproblem_kernel_stats": ([vp, dp, C.POINTER(C.c_long), C.POINTER(C.c_longlong)], C.c_int),
         "mf_gdebug_counters": ([vp, C.c_int, ip], C.c_int),

@@ -89,6 +89,19 @@ struct BKInertia {
     int pos, neg, zero;
 };
 
+// max of M values as a tree of fmax (log2 M dependent steps)
+template <int M>
+__device__ __forceinline__ double tree_max(const double (&v)[M]) {
+    double t[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) t[i] = v[i];
+#pragma unroll
+    for (int st = 1; st < M; st *= 2)
+#pragma unroll
+        for (int i = 0; i + st < M; i += 2 * st) t[i] = fmax(t[i], t[i + st]);
+    return t[0];
+}
+
 // perm/piv: LDS int arrays of length >= m.
 template <int LD>
 __device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm, int *piv, int k0 = 0,
@@ -226,17 +239,20 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
         double cv[M];
 #pragma unroll
         for (int i = 0; i < M; i++) cv[i] = A[i * LD + k];
-        double colmax = 0.0;
-        int imax = k;
-#pragma unroll
-        for (int i = 1; i < M; i++) {
-            const double a = (i > k) ? fabs(cv[i]) : 0.0;
-            if (a > colmax) { colmax = a; imax = i; }
-        }
+        // the first row attaining the column maximum (the wave's argmax; k when the column is zero), by a tree of
+        // fmax and one mask instead of a dependent compare-and-select chain
+        double av[M];
         double absakk = 0.0;
 #pragma unroll
-        for (int i = 0; i < M; i++)
+        for (int i = 0; i < M; i++) {
+            av[i] = (i > k) ? fabs(cv[i]) : 0.0;
             if (i == k) absakk = fabs(cv[i]);
+        }
+        const double colmax = tree_max(av);
+        unsigned hit = 0;
+#pragma unroll
+        for (int i = 1; i < M; i++) hit |= (i > k && av[i] == colmax) ? 1u << i : 0u;
+        const int imax = colmax > 0.0 ? __builtin_ctz(hit) : k;
         int kstep = 1, kp = k;
         if (fmax(absakk, colmax) == 0.0) {
             in.zero++;
@@ -248,15 +264,16 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
         if (absakk >= alpha * colmax) {
             kp = k;
         } else {
-            double rv[M];
+            double rv[M], ra[M];
 #pragma unroll
             for (int j = 0; j < M; j++) rv[j] = A[imax * LD + j];
-            double rowmax = 0.0, aii = 0.0;
+            double aii = 0.0;
 #pragma unroll
             for (int j = 0; j < M; j++) {
-                if (j >= k && j != imax) rowmax = fmax(rowmax, fabs(rv[j]));
+                ra[j] = (j >= k && j != imax) ? fabs(rv[j]) : 0.0;
                 if (j == imax) aii = fabs(rv[j]);
             }
+            const double rowmax = tree_max(ra);
             if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
             else if (aii >= alpha * rowmax) kp = imax;
             else { kp = imax; kstep = 2; }
@@ -283,7 +300,7 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
                 const int i = k + 1 + e / t, j = k + 1 + e % t;
                 if (j <= i) {
                     const double ci = A[i * LD + k], cj = A[j * LD + k];
-                    const double val = A[i * LD + j] - (ci * inv) * cj;
+                    const double val = fma(-(ci * inv), cj, A[i * LD + j]);
                     A[i * LD + j] = val;
                     A[j * LD + i] = val;
                 }
@@ -297,7 +314,7 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
             if (lane == 0) piv[k] = 1;
         } else {
             const double a = A[k * LD + k], bb = A[(k + 1) * LD + k], c = A[(k + 1) * LD + k + 1];
-            const double det = a * c - bb * bb;
+            const double det = fma(a, c, -(bb * bb));
             if (det < 0) { in.pos++; in.neg++; }
             else if (det > 0) { if (a + c > 0) in.pos += 2; else in.neg += 2; }
             else in.zero += 2;
@@ -308,8 +325,8 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
                 if (j <= i) {
                     const double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
                     const double c0j = A[j * LD + k], c1j = A[j * LD + k + 1];
-                    const double l0 = c0i * ia + c1i * ib, l1 = c0i * ib + c1i * ic;
-                    const double val = A[i * LD + j] - (l0 * c0j + l1 * c1j);
+                    const double l0 = fma(c0i, ia, c1i * ib), l1 = fma(c0i, ib, c1i * ic);
+                    const double val = A[i * LD + j] - fma(l0, c0j, l1 * c1j);
                     A[i * LD + j] = val;
                     A[j * LD + i] = val;
                 }
@@ -317,8 +334,8 @@ __device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
             wave_lds_sync();
             for (int i = k + 2 + lane; i < M; i += 64) {
                 const double c0i = A[i * LD + k], c1i = A[i * LD + k + 1];
-                A[i * LD + k] = c0i * ia + c1i * ib;
-                A[i * LD + k + 1] = c0i * ib + c1i * ic;
+                A[i * LD + k] = fma(c0i, ia, c1i * ib);
+                A[i * LD + k + 1] = fma(c0i, ib, c1i * ic);
             }
             if (lane == 0) { piv[k] = 2; piv[k + 1] = 0; }
         }
@@ -702,16 +719,16 @@ __device__ __forceinline__ BKInertia bk_factor_regs_piv(double *A, int *perm, in
             continue;
         }
         const int k1 = k + 1 < M ? k + 1 : M - 1;  // (the second column of a 2x2 pivot; never k = M - 1)
-        double colmax = 0.0;
-        int imax = k;
+        // pivot search without a dependent compare-and-select chain: the column maximum by a tree of fmax, then the
+        // first row that attains it (the wave's argmax: smallest index among ties, k when the column is zero)
+        double cv[M];
 #pragma unroll
-        for (int i = k + 1; i < M; i++) {
-            const double v = fabs(readlane_d(a[k], i));
-            if (v > colmax) {
-                colmax = v;
-                imax = i;
-            }
-        }
+        for (int i = 0; i < M; i++) cv[i] = i > k ? fabs(readlane_d(a[k], i)) : 0.0;
+        const double colmax = tree_max(cv);
+        unsigned hit = 0;
+#pragma unroll
+        for (int i = k + 1; i < M; i++) hit |= (cv[i] == colmax) ? 1u << i : 0u;
+        const int imax = colmax > 0.0 ? __builtin_ctz(hit) : k;
         const double absakk = fabs(readlane_d(a[k], k));
         int kstep = 1, kp = k;
         const bool zero = fmax(absakk, colmax) == 0.0;
@@ -719,20 +736,26 @@ __device__ __forceinline__ BKInertia bk_factor_regs_piv(double *A, int *perm, in
             in.zero++;
         } else {
             if (!(absakk >= alpha * colmax)) {
-                double rowmax = 0.0, dmax = 0.0;
+                // (the row index through an empty asm: the compiler would otherwise speculate these readlanes and the
+                // division below out of the branch and pay for them at every step)
+                int ir = imax;
+                __asm__ volatile("" : "+s"(ir));
+                double rv[M], dmax = 0.0;
 #pragma unroll
-                for (int j = k; j < M; j++) {
-                    const double v = readlane_d(a[j], imax);
-                    if (j != imax) rowmax = fmax(rowmax, fabs(v));
-                    else dmax = v;
+                for (int j = 0; j < M; j++) {
+                    const double v = j >= k ? readlane_d(a[j], ir) : 0.0;
+                    rv[j] = (j >= k && j != imax) ? fabs(v) : 0.0;
+                    dmax = j == imax ? v : dmax;
                 }
+                const double rowmax = tree_max(rv);
                 if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
                 else if (fabs(dmax) >= alpha * rowmax) kp = imax;
                 else { kp = imax; kstep = 2; }
             }
-            const int kk = k + kstep - 1;
+            int kk = k + kstep - 1;
             if (kp != kk) {
                 // rows kk <-> kp (two lanes), then columns kk <-> kp (every lane), then perm
+                __asm__ volatile("" : "+s"(kk), "+s"(kp));
 #pragma unroll
                 for (int j = 0; j < M; j++) {
                     const double vkk = readlane_d(a[j], kk), vkp = readlane_d(a[j], kp);
@@ -745,7 +768,8 @@ __device__ __forceinline__ BKInertia bk_factor_regs_piv(double *A, int *perm, in
                 pm = lane == kk ? pp : (lane == kp ? pk : pm);
             }
             if (kstep == 1) {
-                const double d = readlane_d(a[k], k);
+                double d = readlane_d(a[k], k);
+                __asm__ volatile("" : "+s"(d));  // (not speculated into the 2x2 path)
                 if (d > 0) in.pos++;
                 else if (d < 0) in.neg++;
                 else in.zero++;
@@ -767,7 +791,8 @@ __device__ __forceinline__ BKInertia bk_factor_regs_piv(double *A, int *perm, in
                 }
                 if (lane == k) pv = 1;
             } else {
-                const double a2 = readlane_d(a[k], k), b = readlane_d(a[k], k1), c2 = readlane_d(a[k1], k1);
+                double a2 = readlane_d(a[k], k), b = readlane_d(a[k], k1), c2 = readlane_d(a[k1], k1);
+                __asm__ volatile("" : "+s"(a2), "+s"(b), "+s"(c2));  // (not speculated into the 1x1 path)
                 const double det = fma(a2, c2, -(b * b));
                 if (det < 0) { in.pos++; in.neg++; }
                 else if (det > 0) { if (a2 + c2 > 0) in.pos += 2; else in.neg += 2; }
@@ -816,6 +841,142 @@ __device__ __forceinline__ BKInertia bk_factor_regs_piv(double *A, int *perm, in
             }
             wave_lds_sync();
         }
+    }
+    if (lane < M) {
+#pragma unroll
+        for (int j = 0; j < M; j++) A[lane * LD + j] = a[j];
+        perm[lane] = pm;
+        piv[lane] = pv;
+    }
+    wave_lds_sync();
+    return in;
+}
+
+// bk_factor_regs_piv with a runtime step loop: the column of step k is picked from the registers by a select chain,
+// so the step body exists once (about a tenth of the unrolled routine's code).  Same operations, same bits.
+template <int M>
+__device__ __forceinline__ void reg_put(double (&a)[M], int idx, double v, bool on) {
+#pragma unroll
+    for (int j = 0; j < M; j++) a[j] = (on && idx == j) ? v : a[j];
+}
+template <int LD, int M>
+__device__ __forceinline__ BKInertia bk_factor_regs_loop(double *A, int *perm, int *piv) {
+    static_assert(M >= 2 && M <= 64, "one row per lane");
+    const int lane = lane_opaque();
+    const double alpha = (1.0 + sqrt(17.0)) / 8.0;
+    double a[M];
+#pragma unroll
+    for (int j = 0; j < M; j++) a[j] = A[min(lane, M - 1) * LD + j];
+    int pm = lane, pv = 1;
+    BKInertia in{0, 0, 0};
+    bool first = true;
+    int k = 0;
+#pragma unroll 1
+    while (k < M) {
+        double ck = reg_sel(a, k);
+        double cv[M];
+#pragma unroll
+        for (int i = 0; i < M; i++) cv[i] = i > k ? fabs(readlane_d(ck, i)) : 0.0;
+        const double colmax = tree_max(cv);
+        unsigned hit = 0;
+#pragma unroll
+        for (int i = 1; i < M; i++) hit |= (i > k && cv[i] == colmax) ? 1u << i : 0u;
+        const int imax = colmax > 0.0 ? __builtin_ctz(hit) : k;
+        const double absakk = fabs(readlane_d(ck, k));
+        int kstep = 1, kp = k;
+        if (fmax(absakk, colmax) == 0.0) {
+            in.zero++;
+        } else {
+            if (!(absakk >= alpha * colmax)) {
+                double rv[M], dmax = 0.0;
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    const double v = readlane_d(a[j], imax);
+                    rv[j] = (j >= k && j != imax) ? fabs(v) : 0.0;
+                    dmax = j == imax ? v : dmax;
+                }
+                const double rowmax = tree_max(rv);
+                if (absakk >= alpha * colmax * (colmax / rowmax)) kp = k;
+                else if (fabs(dmax) >= alpha * rowmax) kp = imax;
+                else { kp = imax; kstep = 2; }
+            }
+            const int kk = k + kstep - 1;
+            if (kp != kk) {
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    const double vkk = readlane_d(a[j], kk), vkp = readlane_d(a[j], kp);
+                    a[j] = lane == kk ? vkp : (lane == kp ? vkk : a[j]);
+                }
+                const double tk = reg_sel(a, kk), tp = reg_sel(a, kp);
+#pragma unroll
+                for (int j = 0; j < M; j++) a[j] = j == kk ? tp : (j == kp ? tk : a[j]);
+                const int pk = __builtin_amdgcn_readlane(pm, kk), pp = __builtin_amdgcn_readlane(pm, kp);
+                pm = lane == kk ? pp : (lane == kp ? pk : pm);
+            }
+            const bool below = lane > k + kstep - 1 && lane < M;  // rows of the trailing block
+            if (kstep == 1) {
+                ck = reg_sel(a, k);
+                const double d = readlane_d(ck, k);
+                if (d > 0) in.pos++;
+                else if (d < 0) in.neg++;
+                else in.zero++;
+                const double inv = 1.0 / d;
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    const double cj = readlane_d(ck, j);
+                    if (below && j > k) {
+                        if (j <= lane) a[j] = fma(-(ck * inv), cj, a[j]);
+                        else if (!first) a[j] = fma(-(cj * inv), ck, a[j]);
+                    }
+                    if (lane == k && j > k) a[j] = cj * inv;  // row k: the L column mirrored
+                }
+                reg_put(a, k, ck * inv, below);
+                if (lane == k) pv = 1;
+            } else {
+                const double c0 = reg_sel(a, k), c1 = reg_sel(a, k + 1);
+                const double a2 = readlane_d(c0, k), b = readlane_d(c0, k + 1), c2 = readlane_d(c1, k + 1);
+                const double det = fma(a2, c2, -(b * b));
+                if (det < 0) { in.pos++; in.neg++; }
+                else if (det > 0) { if (a2 + c2 > 0) in.pos += 2; else in.neg += 2; }
+                else in.zero += 2;
+                const double ia = c2 / det, ib = -b / det, ic = a2 / det;
+                const double l0 = fma(c0, ia, c1 * ib), l1 = fma(c0, ib, c1 * ic);
+#pragma unroll
+                for (int j = 0; j < M; j++) {
+                    const double c0j = readlane_d(c0, j), c1j = readlane_d(c1, j);
+                    if (below && j >= k + 2) {
+                        if (j <= lane) {
+                            a[j] = a[j] - fma(l0, c0j, l1 * c1j);
+                        } else if (!first) {
+                            const double l0j = fma(c0j, ia, c1j * ib), l1j = fma(c0j, ib, c1j * ic);
+                            a[j] = a[j] - fma(l0j, c0, l1j * c1);
+                        }
+                    }
+                }
+                reg_put(a, k, l0, below);
+                reg_put(a, k + 1, l1, below);
+                if (lane == k) pv = 2;
+                if (lane == k + 1) pv = 0;
+            }
+        }
+        if (first) {
+            // the trailing block symmetric from its lower triangle (as in bk_factor_regs_piv)
+            const int t0 = 1 + (kstep == 2 ? 1 : 0);
+            if (lane < M) {
+#pragma unroll
+                for (int j = 0; j < M; j++)
+                    if (j <= lane) A[lane * LD + j] = a[j];
+            }
+            wave_lds_sync();
+            if (lane >= t0 && lane < M) {
+#pragma unroll
+                for (int j = 1; j < M; j++)
+                    if (j > lane) a[j] = A[j * LD + lane];
+            }
+            wave_lds_sync();
+            first = false;
+        }
+        k += kstep;
     }
     if (lane < M) {
 #pragma unroll

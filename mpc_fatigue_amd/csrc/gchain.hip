@@ -439,9 +439,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         }
         wave_lds_sync();
         CST(3);
-        // the stage block: Bunch-Kaufman in registers (bk_factor_wave's pivoting and arithmetic; in 2 of 3 stages the
-        // q-dot rows' small diagonal against h J_n takes a 2x2 pivot, which the natural-order path cannot)
-        const BKInertia in = bk_factor_regs_piv<LDK, NK>(Ks, perm, piv);
+        // the stage block: natural-order pivots in registers, else Bunch-Kaufman in LDS with unrolled scans (both with
+        // bk_factor_wave's arithmetic and pivoting, bit for bit; in 2 of 3 stages the q-dot rows' small diagonal
+        // against h J_n takes a 2x2 pivot).  Measured per 9 x 9 block, one wavefront (tools/bk_bench.hip): natural
+        // order in registers 5.0k cycles, pivoting 17.8k (bk_factor_fixed) / 17.4k (bk_factor_regs_piv, whose code
+        // is also 33 KB) / 23.5k (bk_factor_wave).
+        BKInertia in;
+        if (!bk_factor_regs<LDK, NK>(Ks, perm, piv, in)) {
+            in = bk_factor_fixed<LDK, NK>(Ks, perm, piv);
+            CST_COUNT(13, 1);
+        }
         CST(4);
         if (in.zero) { CST_COUNT(15, 1); return 2; }
         if (in.pos != NU || in.neg != NET) { CST_COUNT(14, 1); return 1; }
@@ -480,13 +487,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         issue(N - 1, SIa);
         int fr = 0;
 #pragma unroll 1
-        for (int k = N - 1; k >= 0; k -= 2) {
-            fr = stage(k, SIa, SIb, dw, dc);
-            if (fr || k == 0) break;
-            wave_lds_sync();  // (SIa's readers done before the next DMA overwrites it)
-            fr = stage(k - 1, SIb, SIa, dw, dc);
-            if (fr || k == 1) break;
-            wave_lds_sync();
+        for (int k = N - 1; k >= 0; k--) {
+            // (one stage body for both buffers: the waits are explicit, so nothing needs to name the buffer)
+            SI *cur = ((N - 1 - k) & 1) ? &SIb : &SIa, *nxt = ((N - 1 - k) & 1) ? &SIa : &SIb;
+            __asm__ volatile("" : "+v"(cur), "+v"(nxt));
+            fr = stage(k, *cur, *nxt, dw, dc);
+            if (fr) break;
+            wave_lds_sync();  // (the current buffer's readers done before the next DMA overwrites it)
         }
         if (fr == 0) store_factors(0);
         return fr;
@@ -653,9 +660,10 @@ void gchain_kkt(hipStream_t s, const GParams &P, const GArrays &A, int batch) {
 
 // ============================================================== diagnostics
 namespace mf {
-// one 9 x 9 stage block per workgroup factorised twice, by bk_factor_regs_piv (k_gkkt_chain) and by bk_factor_wave
-// (k_gkkt): both factors, perm | piv << 8 per row and the inertia
-template <int M>
+// one 9 x 9 stage block per workgroup factorised twice, by a variant (V = 0 bk_factor_regs_piv, 1 bk_factor_fixed,
+// 2 bk_factor_regs with the bk_factor_fixed fallback, 3 bk_factor_regs_loop) and by bk_factor_wave (k_gkkt): both factors, perm | piv << 8
+// per row and the inertia
+template <int M, int V>
 __global__ __launch_bounds__(64) void k_bk_compare(const double *K, int n, double *outR, double *outW, int *meta) {
     constexpr int LD = M + 1;
     __shared__ double A1[M * LD], A2[M * LD];
@@ -664,7 +672,13 @@ __global__ __launch_bounds__(64) void k_bk_compare(const double *K, int n, doubl
     if (b >= n) return;
     for (int e = lane; e < M * LD; e += 64) A1[e] = A2[e] = K[(size_t)b * M * LD + e];
     __syncthreads();
-    const BKInertia r = bk_factor_regs_piv<LD, M>(A1, p1, v1);
+    BKInertia r;
+    if constexpr (V == 0) r = bk_factor_regs_piv<LD, M>(A1, p1, v1);
+    if constexpr (V == 1) r = bk_factor_fixed<LD, M>(A1, p1, v1);
+    if constexpr (V == 2) {
+        if (!bk_factor_regs<LD, M>(A1, p1, v1, r)) r = bk_factor_fixed<LD, M>(A1, p1, v1);
+    }
+    if constexpr (V == 3) r = bk_factor_regs_loop<LD, M>(A1, p1, v1);
     __syncthreads();
     const BKInertia w = bk_factor_wave<LD>(A2, M, p2, v2);
     __syncthreads();
@@ -684,9 +698,10 @@ __global__ __launch_bounds__(64) void k_bk_compare(const double *K, int n, doubl
 }
 }  // namespace mf
 
-extern "C" int mf_debug_bk_compare(const double *K, int n, double *outR, double *outW, int *meta) {
+extern "C" int mf_debug_bk_compare(const double *K, int n, int variant, double *outR, double *outW, int *meta) {
     constexpr int M = mf::ChainC2::D::NU + mf::ChainC2::D::NET, LD = M + 1;
-    if (!K || !outR || !outW || !meta || n <= 0) return mf::capi_fail(MF_ERR_ARG, "bad argument");
+    if (!K || !outR || !outW || !meta || n <= 0 || variant < 0 || variant > 3)
+        return mf::capi_fail(MF_ERR_ARG, "bad argument");
     double *dK = nullptr, *dR = nullptr, *dW = nullptr;
     int *dm = nullptr;
     const size_t nb = (size_t)n * M * LD * sizeof(double), mb = (size_t)n * (2 * M + 6) * sizeof(int);
@@ -696,7 +711,10 @@ extern "C" int mf_debug_bk_compare(const double *K, int n, double *outR, double 
     if (e == hipSuccess) e = hipMalloc(&dm, mb);
     if (e == hipSuccess) e = hipMemcpy(dK, K, nb, hipMemcpyHostToDevice);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(mf::k_bk_compare<M>, dim3(n), dim3(64), 0, 0, dK, n, dR, dW, dm);
+        if (variant == 0) hipLaunchKernelGGL((mf::k_bk_compare<M, 0>), dim3(n), dim3(64), 0, 0, dK, n, dR, dW, dm);
+        if (variant == 1) hipLaunchKernelGGL((mf::k_bk_compare<M, 1>), dim3(n), dim3(64), 0, 0, dK, n, dR, dW, dm);
+        if (variant == 2) hipLaunchKernelGGL((mf::k_bk_compare<M, 2>), dim3(n), dim3(64), 0, 0, dK, n, dR, dW, dm);
+        if (variant == 3) hipLaunchKernelGGL((mf::k_bk_compare<M, 3>), dim3(n), dim3(64), 0, 0, dK, n, dR, dW, dm);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpy(outR, dR, nb, hipMemcpyDeviceToHost);

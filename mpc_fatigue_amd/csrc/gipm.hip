@@ -1104,7 +1104,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             }
 #else
             if constexpr (NET <= 2) {
-                if (!bk_factor_regs<LDK, NK>(Ks, perm, piv, in)) in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
+                if (!bk_factor_regs<LDK, NK>(Ks, perm, piv, in)) in = bk_factor_fixed<LDK, NK>(Ks, perm, piv);
             } else {
                 // many constraint rows (Centauro): the control rows in registers (they keep the natural order),
                 // the Schur rows of the constraints by the pivoted LDS routine from column NU

@@ -1,4 +1,5 @@
-"""The register Bunch-Kaufman of k_gkkt_chain (bk_wave.hpp bk_factor_regs_piv) against the LDS one of k_gkkt
+"""The Bunch-Kaufman variants (bk_wave.hpp: bk_factor_regs_piv in registers, bk_factor_fixed in LDS with unrolled scans
+-- k_gkkt_chain's --, bk_factor_regs in natural order with the fixed fallback) against the LDS routine of k_gkkt
 (bk_factor_wave), on the device, bit for bit: the lower triangle (L and D), perm, piv and the inertia.
 
 The stage blocks are built like the C2 chain's K = [[Q_uu, h J_n^T], [h J_n, -dc]] (NU = 7 controls, NET = 2 line rows;
@@ -69,7 +70,8 @@ def _blocks(rng, n):
     return np.ascontiguousarray(np.array(out))
 
 
-def test_register_bunch_kaufman_matches_lds_bit_for_bit():
+@pytest.mark.parametrize("variant", [0, 1, 2, 3], ids=["regs_piv", "lds_fixed", "regs_natural_fixed", "regs_loop"])
+def test_bunch_kaufman_variants_match_lds_bit_for_bit(variant):
     rng = np.random.default_rng(7)
     n = 3000
     K = _blocks(rng, n)
@@ -77,7 +79,7 @@ def test_register_bunch_kaufman_matches_lds_bit_for_bit():
     W = np.zeros_like(K)
     meta = np.zeros((n, 2 * M + 6), np.int32)
     L = _lib.lib()
-    assert _lib.check(L.mf_debug_bk_compare(_lib.dptr(K), n, _lib.dptr(R), _lib.dptr(W), _lib.iptr(meta))) == M
+    assert _lib.check(L.mf_debug_bk_compare(_lib.dptr(K), n, variant, _lib.dptr(R), _lib.dptr(W), _lib.iptr(meta))) == M
     il = np.tril_indices(M)
     lr = R[:, :, :M][:, il[0], il[1]]
     lw = W[:, :, :M][:, il[0], il[1]]

@@ -607,7 +607,9 @@ def test_watchdog_stop_with_failed_search():
     the device's own path is checked: on the first 64 starts of the draw some horizons take it (mf_gdebug_counters;
     measured: starts 25, 44, 50, 52, each then stopping at the 1,500 cap) and every one of them continues to a KKT
     point (status 0, E_0 <= 1e-8) or to one of IPOPT's own outcomes.  The oracle on the same four starts: the path on
-    25, 44 and 52 as well, the cap on 25, 50 and 52, convergence on 44 after 1,456 iterations."""
+    25, 44 and 52 as well, the cap on 25, 50 and 52, convergence on 44 after 1,456 iterations.  Each device outcome is
+    then judged by the oracle's own optimality measures at the device's final primal-dual point (mfg_opts.kkt_at):
+    converged horizons are KKT points of the oracle's problem, capped ones are not."""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
@@ -622,6 +624,17 @@ def test_watchdog_stop_with_failed_search():
                                                                 int(r.iters[b])) for b in hit])
     assert hit, "no horizon took the path"
     assert all(int(r.status[b]) in (0, 1, 4, 5) for b in hit)
+    # the device's outcome judged by the oracle's own functions at the device's final primal-dual point
+    # (mfg_opts.kkt_at): a converged horizon is a KKT point of the oracle's problem (E_0 <= 1e-8, its objective
+    # the device's), a horizon stopped at the cap is not (E_0 > 1e-8 by the oracle's measure as well)
     for b in hit:
+        s_b, d_b = g.point(b)
+        k = G.kkt_at(specs[b], r.w[b], s_b, d_b, bound_relax=1e-8)
+        print(f"start {b}: status {int(r.status[b])}, device E0 {float(r.kkt[b]):.3e}, oracle E0 at the device point "
+              f"{k['E0']:.3e} (pinf {k['pinf']:.1e}), obj {float(r.obj[b]):.10g} / {k['obj']:.10g}")
+        assert abs(k["obj"] - float(r.obj[b])) <= 1e-9 * max(1.0, abs(k["obj"]))
         if int(r.status[b]) == 0:
             assert float(r.kkt[b]) <= 1e-8
+            assert k["E0"] <= 1e-8 and k["pinf"] <= 1e-8
+        elif int(r.status[b]) == 1:
+            assert k["E0"] > 1e-8
