@@ -2374,6 +2374,10 @@ struct mf_gproblem {
     int timing = 0;
     unsigned long long *d_neval = nullptr;
     std::vector<hipEvent_t> ev;
+    // the chain family's Newton step: k_gkkt_chain (main-problem horizons) on the solve stream and the generic k_gkkt
+    // (restoration, least-square multipliers) on this side stream, concurrently (fork / join by events)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     double t_ms[5] = {0, 0, 0, 0, 0};
     long t_launch[5] = {0, 0, 0, 0, 0};
 };
@@ -2634,6 +2638,11 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     if constexpr (ChainEuler<FAM>::value) {
         const char *ev = getenv("MF_CHAIN_KKT");
         chain_kkt = P.filter && P.N <= GCHAIN_NMAX && !(ev && ev[0] == '0');
+        if (chain_kkt && !p->side) {
+            GHIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+            GHIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
+            GHIPCHK(hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming));
+        }
     }
     // the C2 chain's node evaluation direction-major (k_geval_chain; MF_CHAIN_EVAL=0: k_geval, the same lanes)
     bool chain_eval = false;
@@ -2688,10 +2697,16 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             mark(c, 2, 1);
             mark(c, 3, 0);
             As.fast_kkt = 0;
+            hipStream_t ks = s;  // the generic k_gkkt's stream
             if constexpr (ChainEuler<FAM>::value) {
                 if (chain_kkt && !spec) {
+                    // fork: the two kernels take disjoint horizons (k_gkkt skips the ones k_gkkt_chain takes and only
+                    // reads their state's mode / pend, which k_gkkt_chain does not write)
+                    GHIPCHK(hipEventRecord(p->ev_fork, s));
+                    GHIPCHK(hipStreamWaitEvent(p->side, p->ev_fork, 0));
                     gchain_kkt(s, P, A, batch);
                     As.fast_kkt = 1;
+                    ks = p->side;
                 }
             }
             if (spec) {
@@ -2703,10 +2718,14 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             if constexpr (GOcc<FAM>::KKT > 1) {
                 occ = active > kkt_occ_from;
                 if (occ)
-                    hipLaunchKernelGGL((k_gkkt_occ<FAM, GOcc<FAM>::KKT>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P,
+                    hipLaunchKernelGGL((k_gkkt_occ<FAM, GOcc<FAM>::KKT>), dim3(batch), dim3(64), 0, ks, M0, M1, F0, F1, P,
                                        As, batch);
             }
-            if (!occ) hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, s, M0, M1, F0, F1, P, As, batch);
+            if (!occ) hipLaunchKernelGGL(k_gkkt<FAM>, dim3(batch), dim3(64), 0, ks, M0, M1, F0, F1, P, As, batch);
+            if (ks != s) {  // join
+                GHIPCHK(hipEventRecord(p->ev_join, ks));
+                GHIPCHK(hipStreamWaitEvent(s, p->ev_join, 0));
+            }
             mark(c, 3, 1);
             mark(c, 4, 0);
             bool occ_ls = false;
@@ -2896,6 +2915,9 @@ extern "C" void mf_gproblem_free(mf_gproblem *p) {
     if (!p) return;
     gfree_ws(p);
     for (auto e : p->ev) (void)hipEventDestroy(e);
+    if (p->ev_fork) (void)hipEventDestroy(p->ev_fork);
+    if (p->ev_join) (void)hipEventDestroy(p->ev_join);
+    if (p->side) (void)hipStreamDestroy(p->side);
     if (p->d_neval) (void)hipFree(p->d_neval);
     for (double *d : {p->d_ulo, p->d_uhi, p->d_clo, p->d_chi, p->d_ulo_r, p->d_uhi_r, p->d_clo_r, p->d_chi_r})
         if (d) (void)hipFree(d);
