@@ -364,6 +364,13 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     constexpr int NIA2 = NI > 0 ? NI : 1, NMA = NM > 0 ? NM : 1;
     __shared__ double JIs[NIA2 * NV], JMs[NMA * NV];
     __shared__ int fixs[NU], acts[NIA2];
+    // the stage's bound rows (u_lo, u_hi, c_lo, c_hi) and slack-row vectors (y_i, Sigma_s, grad_s, r_i, the elastic
+    // rows' correction and Sigma_p, Sigma_n) staged by LDS-DMA with the record parts, so that a stage's operands
+    // arrive in one memory round trip: a plain load feeding an LDS store makes the wave wait (vmcnt, in order) for
+    // everything issued before it, one more round trip per such loop.  The flags and weights are formed after it.
+    constexpr int SL_YI = 0, SL_SS = NIA2, SL_GS = 2 * NIA2, SL_RI = 3 * NIA2, SL_RR = 4 * NIA2, SL_SP = 5 * NIA2,
+                  SL_SN = 6 * NIA2, SL_END = 7 * NIA2;
+    __shared__ double Bnd[2 * NU + 2 * NIA2], Sl[SL_END], PPd[2 * (NU + NET)];
     // stage vectors (stage_vec): barrier Sigma of the stage's x / u / slack rows (factor), and for the
     // direction's backward pass grad L_k, the barrier gradients, lambda_k, lambda_{k-1}, y_e,k, the slack
     // weights w_q, rd_k, re_k, re_{k+1} and J_E of node k
@@ -890,6 +897,21 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
     // objective gradient is left out
     const bool lsm = flt && st.pend == GP_LSM;
     auto rdiag = [&](size_t r) __attribute__((always_inline)) -> double { return rsm ? 1.0 / Spr[r] + 1.0 / Snr[r] : 0.0; };
+    // the bound rows of stage k into LDS (LDS-DMA; flags_in forms fixs / acts from them once they have arrived)
+    auto bounds_in = [&](int k) __attribute__((always_inline)) {
+        glds_copy(Bnd, ulo + (size_t)k * NU, NU);
+        glds_copy(Bnd + NU, uhi + (size_t)k * NU, NU);
+        if (NI > 0) {
+            glds_copy(Bnd + 2 * NU, clo + (size_t)k * NI, NI);
+            glds_copy(Bnd + 2 * NU + NIA2, chi + (size_t)k * NI, NI);
+        }
+    };
+    auto flags_in = [&](bool with_acts) __attribute__((always_inline)) {
+        for (int c = lane; c < NU; c += 64) fixs[c] = (gb(Bnd[c]) && Bnd[c] == Bnd[NU + c]) ? 1 : 0;
+        if (with_acts)
+            for (int q = lane; q < NI; q += 64) acts[q] = (gb(Bnd[2 * NU + q]) || gb(Bnd[2 * NU + NIA2 + q])) ? 1 : 0;
+        wave_lds_sync();
+    };
     // stage k's A, B, J_I, J_M (and W into Hs), J_E of node k+1, the fixed-control and active-row flags
     auto stage_in = [&](int k, bool withW) __attribute__((always_inline)) {
         const double *rk = R(k);
@@ -902,8 +924,7 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
         if (en && NE > 0) glds_copy(Jn, R(k + 1) + D::O_JE, NE * NX);
         for (int e = lane; e < NEA * NX; e += 64)
             if (!(en && e < NE * NX)) Jn[e] = 0.0;
-        for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
-        for (int q = lane; q < NI; q += 64) acts[q] = cact(k, q) ? 1 : 0;
+        bounds_in(k);
     };
     // IPOPT's restoration problem puts elastic p, n on the dynamics rows too (oracle/mf_ocp.c ric_relax): row k reads
     // dx_{k+1} = A dx_k + B du_k + r - D_r dlam_k, D_r = 1/Sp + 1/Sn.  With L = I + P_{k+1} D_r (LU, partial
@@ -962,13 +983,19 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             if (rlx && relax_stage(k, en)) return 1;
             for (int e = lane; e < NX * NX; e += 64) Pg[(size_t)k * NX * NX + e] = Ps[e];
             stage_in(k, true);
-            for (int j = lane; j < NX; j += 64) Vs[V_SX + j] = Sx[k * NX + j];
-            for (int c = lane; c < NU; c += 64) Vs[V_SU + c] = Su[k * NU + c];
-            for (int q = lane; q < NI; q += 64) Vs[V_SS + q] = Ss[k * NIA + q];
+            glds_copy(Vs + V_SX, Sx + k * NX, NX);
+            glds_copy(Vs + V_SU, Su + k * NU, NU);
+            if (NI > 0) glds_copy(Vs + V_SS, Ss + k * NIA, NI);
+            if (rsm && NI > 0) {
+                glds_copy(Sl + SL_SP, Spr + (size_t)k * NIA, NI);
+                glds_copy(Sl + SL_SN, Snr + (size_t)k * NIA, NI);
+            }
             gsync();
+            flags_in(true);
             for (int q = lane; q < NI; q += 64) {
                 const double sg = Vs[V_SS + q] + dw;
-                Dds[q] = acts[q] ? sg / (1.0 + (dc + rdiag((size_t)k * NIA + q)) * sg) : 0.0;
+                const double rdq = rsm ? 1.0 / Sl[SL_SP + q] + 1.0 / Sl[SL_SN + q] : 0.0;  // rdiag(k NIA + q)
+                Dds[q] = acts[q] ? sg / (1.0 + (dc + rdq) * sg) : 0.0;
             }
             if (lsm)
                 for (int e = lane; e < NV * NV; e += 64) Hs[e] = (e / NV == e % NV) ? 1.0 : 0.0;
@@ -1090,19 +1117,8 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             // natural-order pivots in registers (the common case), the pivoted LDS factorisation otherwise
             BKInertia in;
             // (stage blocks with at most two constraint rows: with more, the Schur rows usually need pivoting)
-#ifdef MF_GSTAMPS
-            // diagnostic: the register path on every family, and where it stops (slot 27: sum of the failing
-            // column, 28: failures, 29: failures in the control rows)
-            {
-                int fc = -1;
-                if (!bk_factor_regs<LDK, NK>(Ks, perm, piv, in, &fc)) {
-                    in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
-                    GSTAMP_COUNT(27, fc);
-                    GSTAMP_COUNT(28, 1);
-                    GSTAMP_COUNT(29, fc < NU ? 1 : 0);
-                }
-            }
-#else
+            // (the stamps build runs this same path: its round-5 variant, the whole block in registers on every family,
+            // was the only code difference of that build and the r05c fault came with it)
             if constexpr (NET <= 2) {
                 if (!bk_factor_regs<LDK, NK>(Ks, perm, piv, in)) in = bk_factor_fixed<LDK, NK>(Ks, perm, piv);
             } else {
@@ -1112,7 +1128,6 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (bk_factor_regs<LDK, NK, NU>(Ks, perm, piv, in0)) in = bk_factor_wave<LDK>(Ks, NK, perm, piv, NU, in0);
                 else in = bk_factor_wave<LDK>(Ks, NK, perm, piv);
             }
-#endif
             GSTAMP(12);
             if (in.zero) return 2;
             if (in.pos != NU || in.neg != NET) return 1;
@@ -1178,18 +1193,22 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (k > 0) glds_copy(Vs + V_LP, lam + (k - 1) * NX, NX);
                 if (k + 1 < N) glds_copy(Vs + V_RN, re + (k + 1) * NET, NEA);
                 if (eqon(k) && NE > 0) glds_copy(Vs + V_JE, rk + D::O_JE, NE * NX);
+                glds_copy(PPd, kst + NK * LDK, 2 * NK);  // perm, piv (stored as doubles)
+                if (NI > 0) {
+                    glds_copy(Sl + SL_YI, yi + (size_t)k * NIA, NI);
+                    glds_copy(Sl + SL_SS, Ss + (size_t)k * NIA, NI);
+                    glds_copy(Sl + SL_GS, gs + (size_t)k * NIA, NI);
+                    glds_copy(Sl + SL_RI, ri + (size_t)k * NIA, NI);
+                    if (rsm) {
+                        glds_copy(Sl + SL_RR, rowr + (size_t)k * NIA, NI);
+                        glds_copy(Sl + SL_SP, Spr + (size_t)k * NIA, NI);
+                        glds_copy(Sl + SL_SN, Snr + (size_t)k * NIA, NI);
+                    }
+                }
                 if (rlx) {  // elastic dynamics rows: the stage's LU of I + P D_r and permutation, J~ (Hs rows < NX: free)
                     glds_copy(Hs, LUb + (size_t)k * (NX * NX + NX), NX * NX + NX);
                     if (en && NE > 0) glds_copy(Jts, Jtb + (size_t)k * NEA * NX, NE * NX);
                     for (int j = lane; j < NX; j += 64) Drs[j] = rdiag(NRD + (size_t)k * NX + j);
-                }
-                for (int e = lane; e < NK; e += 64) {
-                    perm[e] = (int)kst[NK * LDK + e];
-                    piv[e] = (int)kst[NK * LDK + NK + e];
-#ifdef MF_GCHK
-                    if (perm[e] < 0 || perm[e] >= NK) { GCHK_BAD(1, perm[e]); perm[e] = e; }
-                    if (piv[e] < 0 || piv[e] > 2) { GCHK_BAD(2, piv[e]); piv[e] = 1; }
-#endif
                 }
             }
             GCHK(21, k);
@@ -1199,6 +1218,16 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 if (k + 1 >= N) Vs[V_RN + ee] = 0.0;
             for (int e = lane; e < NEA * NX; e += 64)
                 if (!(eqon(k) && e < NE * NX)) Vs[V_JE + e] = 0.0;
+            gsync();  // the stage's operands have arrived (one round trip)
+            flags_in(true);
+            for (int e = lane; e < NK; e += 64) {
+                perm[e] = (int)PPd[e];
+                piv[e] = (int)PPd[NK + e];
+#ifdef MF_GCHK
+                if (perm[e] < 0 || perm[e] >= NK) { GCHK_BAD(1, perm[e]); perm[e] = e; }
+                if (piv[e] < 0 || piv[e] > 2) { GCHK_BAD(2, piv[e]); piv[e] = 1; }
+#endif
+            }
             if (rlx) {  // p~ = L^-1 p_{k+1} (stored for the forward sweep), rd + the elastic rows' correction
                 for (int j = lane; j < NX; j += 64) {
                     pix[j] = (int)Hs[NX * NX + j];
@@ -1214,17 +1243,17 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                 wave_lds_sync();
                 for (int j = lane; j < NX; j += 64) pvg[k * NX + j] = ptv[j];
             }
-            // slack-row weights of the stage (vx: the J_I^T w term)
+            // slack-row weights of the stage (vx: the J_I^T w term), from the staged rows
             for (int q = lane; q < NI; q += 64) {
-                const int i = k * NIA + q;
-                double w = yi[i];
-                if (cact(k, q)) {
-                    const double sg = Ss[i] + dw, Dd = sg / (1.0 + (dc + rdiag(i)) * sg);
-                    w += Dd * (ri[i] + (rsm ? rowr[i] : 0.0) + (gs[i] - yi[i]) / sg);
+                double w = Sl[SL_YI + q];
+                if (acts[q]) {
+                    const double rdq = rsm ? 1.0 / Sl[SL_SP + q] + 1.0 / Sl[SL_SN + q] : 0.0;  // rdiag(k NIA + q)
+                    const double sg = Sl[SL_SS + q] + dw, Dd = sg / (1.0 + (dc + rdq) * sg);
+                    w += Dd * (Sl[SL_RI + q] + (rsm ? Sl[SL_RR + q] : 0.0) + (Sl[SL_GS + q] - Sl[SL_YI + q]) / sg);
                 }
                 Vs[V_W + q] = w;
             }
-            gsync();
+            wave_lds_sync();
             GSTAMP(19);
             for (int a = lane; a < NV; a += 64) {
                 const bool fa = a < NX ? (k == 0) : fixs[a - NX];
@@ -1312,8 +1341,9 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             if (rlx && en && NE > 0) glds_copy(Jts, Jtb + (size_t)k * NEA * NX, NE * NX);
             for (int e = lane; e < NEA * NX; e += 64)
                 if (!(en && e < NE * NX)) Jn[e] = 0.0;
-            for (int c = lane; c < NU; c += 64) fixs[c] = ufix(k * NU + c) ? 1 : 0;
+            bounds_in(k);
             gsync();
+            flags_in(false);
             for (int a = lane; a < NK; a += 64) {
                 double acc = zv[a];
                 for (int j = 0; j < NX; j++) acc += Kf[a * NX + j] * dxs[j];
@@ -1327,14 +1357,14 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
                     vx[j] += rowr[NRD + (size_t)k * NX + j];
                     drj = rdiag(NRD + (size_t)k * NX + j);
                 }
-            gsync();
+            wave_lds_sync();
             for (int j = lane; j < NX; j += 64) {
                 double acc = vx[j];
                 for (int l = 0; l < NX; l++) acc += Ab[j * NX + l] * dxs[l];
                 for (int c = 0; c < NU; c++) acc += Bb[j * NU + c] * duv[c];
                 dxn[j] = acc;
             }
-            gsync();
+            wave_lds_sync();
             for (int j = lane; j < NX; j += 64) {
                 // dlam = P~ z + p~ + J~^T dy_s, dx_{k+1} = z - D_r dlam (hard rows: P, p, J_n, D_r = 0)
                 double acc = tv[j];
@@ -1349,10 +1379,11 @@ __device__ __forceinline__ void giter_phase(const DevModel *M0, const DevModel *
             if (k + 1 < N)
                 for (int ee = lane; ee < NEA; ee += 64) dye[(k + 1) * NET + ee] = (en && ee < NE) ? duv[NU + ee] : 0.0;
             for (int m = lane; m < NM; m += 64) dye[k * NET + NEA + m] = duv[NU + NEA + m];
-            gsync();
+            wave_lds_sync();
             for (int j = lane; j < NX; j += 64) dxs[j] = rlx ? dxn[j] - drj * dlj : dxn[j];
-            gsync();
+            wave_lds_sync();
         }
+        gsync();  // (the sweep's global stores retired before anything reads them back)
         GSTAMP(17);
         GCHK(24, 0);
         // slack rows and bound multipliers
@@ -2190,13 +2221,16 @@ __global__ __launch_bounds__(64) void k_gspec(const DevModel *M0, const DevModel
     giter_phase<FAM, 3, true>(M0, M1, F0, F1, P, A, batch);
 }
 // the running horizons (at most A.spec_max, the host's condition for launching k_gspec) listed for k_gspec
-__global__ __launch_bounds__(1024) void k_gspec_list(GArrays A, int batch) {
+// nonfast: only the horizons k_gkkt_chain leaves to k_gkkt (restoration phase, pending actions): their tries run
+// concurrently while the chain kernel takes the others
+__global__ __launch_bounds__(1024) void k_gspec_list(GArrays A, int batch, int nonfast) {
     __shared__ int cnt;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
     for (int b = threadIdx.x; b < batch; b += blockDim.x) {
         int s = -1;
-        if (A.st[b].status == GS_RUNNING) {
+        const GState &g = A.st[b];
+        if (g.status == GS_RUNNING && !(nonfast && g.mode == 0 && g.pend == GP_NONE)) {
             s = atomicAdd(&cnt, 1);
             if (s >= A.spec_max) s = -1;
             else A.slist[s] = b;
@@ -2634,10 +2668,13 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     GArrays As = A;  // k_gkkt's view: spec_of set while k_gspec runs
     // the chain family's main-problem Newton step by k_gkkt_chain (IPOPT mode, not while k_gspec runs);
     // MF_CHAIN_KKT=0 in the environment keeps k_gkkt for every horizon (A/B diagnostics)
-    bool chain_kkt = false;
+    bool chain_kkt = false, chain_rspec = false;
     if constexpr (ChainEuler<FAM>::value) {
         const char *ev = getenv("MF_CHAIN_KKT");
         chain_kkt = P.filter && P.N <= GCHAIN_NMAX && !(ev && ev[0] == '0');
+        const char *er = getenv("MF_CHAIN_RSPEC");
+        // (MF_CHAIN_RSPEC=1: the left-over horizons' inertia tries concurrently as well; measured no faster, DESIGN s.9)
+        chain_rspec = chain_kkt && spec_ok && A.spec_max > 0 && (er && er[0] == '1');
         if (chain_kkt && !p->side) {
             GHIPCHK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
             GHIPCHK(hipEventCreateWithFlags(&p->ev_fork, hipEventDisableTiming));
@@ -2707,10 +2744,17 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
                     gchain_kkt(s, P, A, batch);
                     As.fast_kkt = 1;
                     ks = p->side;
+                    if (chain_rspec) {
+                        // the left-over horizons' inertia tries concurrently as well (k_gspec on the side stream)
+                        hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, ks, A, batch, 1);
+                        hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * A.spec_max), dim3(64), 0, ks, M0, M1, F0, F1, P,
+                                           A, batch);
+                        As.spec_of = A.spec_of;
+                    }
                 }
             }
             if (spec) {
-                hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch);
+                hipLaunchKernelGGL(k_gspec_list, dim3(1), dim3(1024), 0, s, A, batch, 0);
                 hipLaunchKernelGGL(k_gspec<FAM>, dim3(GNSPEC * std::min(active, A.spec_max)), dim3(64), 0, s, M0, M1, F0,
                                    F1, P, A, batch);
             }
