@@ -228,7 +228,7 @@ __device__ __forceinline__ BKInertia bk_factor_wave(double *A, int m, int *perm,
 // Same factorisation with a compile-time size M <= 64: the pivot scans are unrolled, so their
 // LDS reads issue back to back instead of one dependent round trip per candidate.
 template <int LD, int M>
-__device__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
+__device__ __forceinline__ BKInertia bk_factor_fixed(double *A, int *perm, int *piv) {
     const int lane = lane_opaque();
     const double alpha = (1.0 + sqrt(17.0)) / 8.0;
     BKInertia in{0, 0, 0};

@@ -202,8 +202,8 @@ template <int NV, int NI, int NE, int NX, int NU, int NIA, int NET, int NEA> str
                          LK = YI + NIA, LP = LK + NX, YE = LP + NX, RD = YE + NET, RI = RD + NX, RN = RI + NIA,
                          END = RN + NEA;
     double W[NV * NV], JI[NI * NV], GL[NV], Jn[NE * NX], JE[NE * NX], V[END];
-    // LDS-DMA instructions of one stage's copy (glds_copy: one per 64 dwords of each piece)
-    static constexpr int nc(int nd) { return (2 * nd + 63) / 64; }
+    // LDS-DMA instructions of one stage's copy (glds_copy)
+    static constexpr int nc(int nd) { return glds_instr(nd); }
     static constexpr int DMA = nc(NV * NV) + nc(NI * NV) + nc(NV) + 2 * nc(NE * NX) + 5 * nc(NX) + 2 * nc(NU) +
                                4 * nc(NIA) + nc(NET) + nc(NEA);
 };
@@ -274,12 +274,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // of a stage's results are deferred to the next stage, after its wait (stores issued between two stages' copies
     // would have to retire before the second wait).  Nothing writes into a buffer after its DMA.
     using SI = ChainStageIn<NV, NI, NE, NX, NU, NIA, NET, NEA>;
-    __shared__ SI SIa, SIb;
+    __shared__ SI SIb2[2];  // (indexed by a runtime slot: every access stays an LDS access, ds_read / ds_write)
     __shared__ double Ks[NK * LDK], Bm[NK * NR], Rh[NK * NX], Qx[NX * NX], Ps[NX * NX], T2[NX * NX];
     __shared__ double Dd[NIA], wq[NIA], vx[NX], tv[NX], pvs[NX], zv[NK];
     __shared__ int perm[NK], piv[NK];
 
-    auto issue = [&](int k, SI &T) __attribute__((always_inline)) {
+    auto issue = [&](int k, int slot) __attribute__((always_inline)) {
+        SI &T = SIb2[slot];
         const int lane = lane_opaque();
         const double *rk = R(k), *rn = k + 1 < N ? R(k + 1) : rk;
         glds_copy(T.W, rk + D::O_W, NV * NV, lane);
@@ -313,10 +314,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
     // one stage of the backward sweep from the inputs in C, prefetching stage k - 1's into Nx (0 ok, 1 wrong inertia,
     // 2 singular block)
-    auto stage = [&](int k, const SI &C, SI &Nx, double dw, double dc) __attribute__((always_inline)) -> int {
+    auto stage = [&](int k, int slot, double dw, double dc) __attribute__((always_inline)) -> int {
+        const SI &C = SIb2[slot];
         CST_COUNT(10, 1);
         if (k >= 1) {
-            issue(k - 1, Nx);
+            issue(k - 1, slot ^ 1);
             wait_vm<SI::DMA>();
         } else {
             wait_vm<0>();
@@ -484,14 +486,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         wave_mem_sync();  // (a failed try may have left a prefetch in flight)
         CST_COUNT(9, 1);
         CST(0);
-        issue(N - 1, SIa);
+        issue(N - 1, 0);
         int fr = 0;
 #pragma unroll 1
         for (int k = N - 1; k >= 0; k--) {
             // (one stage body for both buffers: the waits are explicit, so nothing needs to name the buffer)
-            SI *cur = ((N - 1 - k) & 1) ? &SIb : &SIa, *nxt = ((N - 1 - k) & 1) ? &SIa : &SIb;
-            __asm__ volatile("" : "+v"(cur), "+v"(nxt));
-            fr = stage(k, *cur, *nxt, dw, dc);
+            fr = stage(k, (N - 1 - k) & 1, dw, dc);
             if (fr) break;
             wave_lds_sync();  // (the current buffer's readers done before the next DMA overwrites it)
         }
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     // forward sweep: du_k = k_k + Kf dx_k, dx_{k+1} = r_d + dx_k + h du_qd, dlam_k = p_{k+1} + P_{k+1} dx_{k+1} +
     // J_n^T dy_{k+1}
     __shared__ double dxs[NX], dxn[NX], duv[NK];
-    double *Jn = SIa.Jn;  // (the backward sweep's buffers are free now)
+    double *Jn = SIb2[0].Jn;  // (the backward sweep's buffers are free now)
     wave_mem_sync();
     for (int j = lane; j < NX; j += 64) { dxs[j] = 0.0; dx[j] = 0.0; }
     for (int ee = lane; ee < NEA; ee += 64) dye[ee] = 0.0;

@@ -151,18 +151,25 @@ __device__ __forceinline__ void gsync() {
     __syncthreads();
 }
 
-// nd contiguous doubles global -> LDS by LDS-DMA (global_load_lds_dword: no VGPR destination, every
-// instruction of the copy in flight at once; the next gsync()'s vmcnt(0) retires them).  Dword granularity:
-// the record fields are only 8-byte aligned.  The LDS destination of one instruction is the wave-uniform
-// base + 4 x lane, so lanes past the end are masked off (they would write beyond the array).
+// nd contiguous doubles global -> LDS by LDS-DMA (no VGPR destination, every instruction of the copy in flight at
+// once; the next gsync()'s vmcnt(0) retires them).  16 bytes per lane (global_load_lds_dwordx4: 128 doubles per
+// wave-instruction; 8-byte-aligned sources and destinations are fine, tools/glds16_check.hip), the last double of an
+// odd count by two 4-byte lanes.  The LDS destination of one instruction is the wave-uniform base + size x lane, so
+// lanes past the end are masked off (they would write beyond the array).  Instructions issued: glds_instr(nd).
+__host__ __device__ constexpr int glds_instr(int nd) { return (nd / 2 + 63) / 64 + (nd & 1); }
 __device__ __forceinline__ void glds_copy(double *lds, const double *src, int nd, int lane = threadIdx.x) {
-    const int nw = 2 * nd;
-    const unsigned *s = reinterpret_cast<const unsigned *>(src);
-    unsigned *d = reinterpret_cast<unsigned *>(lds);
-    for (int t = 0; t < nw; t += 64)
-        if (t + lane < nw)
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(s + t + lane),
-                                             (__attribute__((address_space(3))) void *)(d + t), 4, 0, 0);
+    const int n2 = nd & ~1;
+    for (int t = 0; t < n2; t += 128)
+        if (t + 2 * lane < n2)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(src + t + 2 * lane),
+                                             (__attribute__((address_space(3))) void *)(lds + t), 16, 0, 0);
+    if (nd & 1) {
+        const unsigned *s4 = reinterpret_cast<const unsigned *>(src + n2);
+        unsigned *d4 = reinterpret_cast<unsigned *>(lds + n2);
+        if (lane < 2)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(s4 + lane),
+                                             (__attribute__((address_space(3))) void *)d4, 4, 0, 0);
+    }
 }
 
 // first NJ joints of a DevModel in LDS
