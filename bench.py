@@ -181,8 +181,9 @@ def main() -> int:
     ap.add_argument("--generic-batch", type=int, default=4096,
                     help="starts per generic-solver figure (the C3 figure is set by a few starts that run to the "
                          "cap at single-horizon latency, so a larger batch amortises that tail)")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="independent steps in flight (own workspace, stream and host thread each)")
+    ap.add_argument("--inflight", type=int, default=3,
+                    help="independent steps in flight (own workspace, stream and host thread each; measured r06zb: "
+                         "2 -> 1,291, 3 -> 1,496, 4 -> 1,491 horizons/s)")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="HIP hardware queues of this process (GPU_MAX_HW_QUEUES, set before the runtime starts, "
                          "over any exported value; 0 = keep the exported value)")
