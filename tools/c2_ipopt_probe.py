@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--verbose", type=int, default=1)
     ap.add_argument("--timing", action="store_true", help="per-phase HIP-event timing of the (first) timed solve")
     ap.add_argument("--cstamps", action="store_true", help="k_gkkt_chain phase cycles (diagnostic build)")
+    ap.add_argument("--no-spec", action="store_true", help="no concurrent inertia tries in the tail (inertia_spec -1)")
     a = ap.parse_args()
     if a.cstamps:
         os.environ["MF_LIB"] = "libmpcfatigue_cstamps.so"
@@ -50,6 +51,8 @@ def main():
            "kkt": torch.empty(B, dtype=torch.float64, device=dev), "obj": torch.empty(B, dtype=torch.float64, device=dev)}
     ptr = {k: v.data_ptr() for k, v in out.items()}
     kw = dict(init_zero=True, filter=True, bound_relax=1e-8, max_iter=a.max_iter, max_soc=4)
+    if a.no_spec:
+        kw["inertia_spec"] = -1
     s = torch.cuda.current_stream(dev).cuda_stream
     g.solve_dev(x.data_ptr(), None, None, l.data_ptr(), B, ptr, stream=s, **dict(kw, max_iter=1))
     torch.cuda.synchronize()
