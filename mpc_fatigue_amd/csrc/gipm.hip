@@ -2693,6 +2693,12 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
     // the occupancy variants while more horizons run than the default kernels hold (four per CU; measured on the C2
     // leg: launches at ~1000 running horizons take the same time with either k_gkkt, fewer run faster without spills)
     int kkt_occ_from = batch;
+    // MF_GLS_OCC=0 in the environment keeps the default k_gls at every running count (A/B diagnostics)
+    const char *egl = getenv("MF_GLS_OCC");
+    const bool gls_occ_on = !(egl && egl[0] == '0');
+    // MF_GKKT_OCC=0: the default k_gkkt at every running count
+    const char *egk = getenv("MF_GKKT_OCC");
+    const bool gkkt_occ_on = !(egk && egk[0] == '0');
     if constexpr (GOcc<FAM>::KKT > 1) {
         int dev = 0, ncu = 0;
         GHIPCHK(hipGetDevice(&dev));
@@ -2760,7 +2766,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             }
             bool occ = false;
             if constexpr (GOcc<FAM>::KKT > 1) {
-                occ = active > kkt_occ_from;
+                occ = gkkt_occ_on && active > kkt_occ_from;
                 if (occ)
                     hipLaunchKernelGGL((k_gkkt_occ<FAM, GOcc<FAM>::KKT>), dim3(batch), dim3(64), 0, ks, M0, M1, F0, F1, P,
                                        As, batch);
@@ -2774,7 +2780,7 @@ static int gsolve_core(mf_gproblem *p, int batch, const double *d_x0, const doub
             mark(c, 4, 0);
             bool occ_ls = false;
             if constexpr (GOcc<FAM>::LS > 1) {
-                occ_ls = active > kkt_occ_from;
+                occ_ls = gls_occ_on && active > kkt_occ_from;
                 if (occ_ls && P.filter)
                     hipLaunchKernelGGL((k_gls_occ<FAM, true, GOcc<FAM>::LS>), dim3(batch), dim3(64), 0, s, M0, M1, F0, F1,
                                        P, A, batch);
