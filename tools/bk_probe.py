@@ -15,7 +15,7 @@ K = _blocks(np.random.default_rng(7), n)
 R = np.zeros_like(K)
 W = np.zeros_like(K)
 meta = np.zeros((n, 2 * M + 6), np.int32)
-_lib.check(_lib.lib().mf_debug_bk_compare(_lib.dptr(K), n, _lib.dptr(R), _lib.dptr(W), _lib.iptr(meta)))
+_lib.check(_lib.lib().mf_debug_bk_compare(_lib.dptr(K), n, 0, _lib.dptr(R), _lib.dptr(W), _lib.iptr(meta)))
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 np.savez(os.path.join(ROOT, "gpurun_out", "bk_probe.npz"), K=K, R=R, W=W, meta=meta)
 print("ok")
