@@ -367,6 +367,17 @@ def main() -> int:
             t1024, c1024, _ = timed(1024, 1)
             result["c5_shard_1024"] = {"value": c1024 / t1024, "unit": "horizons/s", "ms_per_step": t1024 * 1e3,
                                        "converged": c1024, "note": "first 1024 horizons of the batch, one step alone"}
+            # the same shard as each rank of an 8-GPU C5 run solves it (--c5 at N = 8): steps in flight
+            K1 = 4 * inflight
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            run_steps(K1, nb=1024)
+            torch.cuda.synchronize(dev)
+            tk = time.perf_counter() - t
+            ck = int((out["status"][:1024] == 0).sum().item())
+            result["c5_shard_1024"]["inflight"] = {
+                "value": ck * K1 / tk, "steps": K1, "steps_in_flight": inflight, "ms_per_step": tk / K1 * 1e3,
+                "note": "1024 horizons per step, the bench's steps in flight (the per-rank load of C5 on 8 GPUs)"}
         t1, c1, o1 = timed(1, 3)
         result["single_problem"] = {"ms_per_solve": t1 * 1e3, "converged": c1, "iters": int(o1["iters"][0].item()),
                                     "note": "horizon 0 of the batch alone, IPOPT mode, median of 3 (host-polled every "
